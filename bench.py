@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""bench.py -- QPs/sec of the batched MI355X QP solver (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): per GPU a batch of 65,536 dense QPs,
+n=16, m=32, fp64, solved by the active-set kernel (qpb_solve) through the
+C-ABI.  Synthetic "conditioned box" family: H = B^T B/(1e3 n)
++ I (the reference generator's P, matrix_ops.c:699-734, shifted), f ~
+U[-1e3,1e3], box |x_i| <= 10 written as a dense A = [I; -I], b = 10 (so the
+solver reads the full dense (H, f, A, b)).  Inputs are generated on the GPU
+and resident in HBM before the timed region.
+
+One step = one qpb_solve launch over the rank's batch.  Multi-GPU: one process
+per GPU (torchrun), QPs sharded by index, no collective in the data path
+(weak scaling); timings are max-reduced over ranks.
+
+Also reported:
+  roofline     -- algorithmic HBM bytes per launch / mean kernel time (HIP
+                  events on the launch stream) vs 8 TB/s
+  cpu_baseline -- the reference's own qp_solvers.c admm() (compiled from
+                  /root/reference by oracle/Makefile, box +-10 compiled in) on
+                  a sample of the same QPs, one process per core, rank 0, N=1
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
+
+
+def bytes_per_qp(n: int, m: int) -> int:
+    """Algorithmic HBM bytes per QP: inputs H n*n, f n, A m*n,
+    b m; outputs x n, lam m, active ceil(m/32) words, status 1 word (fp64 = 8 B)."""
+    return 8 * (n * n + n + m * n + m) + 8 * (n + m) + 4 * ((m + 31) // 32) + 4
+
+
+def make_batch(torch, B: int, n: int, family: str, seed: int, device, box: float = 10.0):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    Bm = (torch.rand((B, n, n), generator=g, device=device, dtype=torch.float64) * 2 - 1) * 1e3
+    H = torch.bmm(Bm.transpose(1, 2), Bm) / (1e3 * n) + torch.eye(n, device=device, dtype=torch.float64)
+    del Bm
+    H = 0.5 * (H + H.transpose(1, 2))
+    f = (torch.rand((B, n), generator=g, device=device, dtype=torch.float64) * 2 - 1) * 1e3
+    if family == "box":
+        eye = torch.eye(n, device=device, dtype=torch.float64)
+        A = torch.cat([eye, -eye], 0).expand(B, 2 * n, n).contiguous()
+        b = torch.full((B, 2 * n), box, device=device, dtype=torch.float64)
+    else:
+        A = torch.randn((B, 2 * n, n), generator=g, device=device, dtype=torch.float64)
+        A = A / A.norm(dim=2, keepdim=True)
+        b = (torch.rand((B, 2 * n), generator=g, device=device, dtype=torch.float64) * 0.9 + 0.1) * box
+    return H.contiguous(), f.contiguous(), A.contiguous(), b.contiguous()
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    lib_path, P, q, seconds, iters = args
+    import ctypes
+
+    import numpy as np
+    L = ctypes.CDLL(lib_path)
+    dp = ctypes.POINTER(ctypes.c_double)
+    x0 = np.zeros_like(q)
+    x = np.zeros_like(q)
+    done = 0
+    chunk = 64
+    t0 = time.perf_counter()
+    i = 0
+    while True:
+        j = min(i + chunk, len(q))
+        L.ref_admm_batch(ctypes.c_uint(j - i), P[i:j].ctypes.data_as(dp), q[i:j].ctypes.data_as(dp),
+                         x0[i:j].ctypes.data_as(dp), ctypes.c_uint(iters), x[i:j].ctypes.data_as(dp))
+        done += j - i
+        i = 0 if j >= len(q) else j
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return done, el
+
+
+def cpu_baseline(H, f, seconds: float, procs: int):
+    """The reference admm() on the same box QPs (uniform box 10 compiled in,
+    config.h:29-30), one forked process per core (the reference is not
+    thread-safe: static pools kmalloc.c:37-42)."""
+    import multiprocessing as mp
+
+    import numpy as np
+    lib = os.path.join(ROOT, "oracle", "_ref", "libqpref_n16_10.so")
+    if not os.path.exists(lib):
+        return {"value": None, "unit": "QPs/s", "cores": 0, "kind": "reference",
+                "sample": "oracle/_ref/libqpref_n16_10.so missing (build with make -C oracle ref)"}
+    P = np.ascontiguousarray(H)
+    q = np.ascontiguousarray(f)
+    per = max(1, len(q) // procs)
+    jobs = [(lib, P[k * per:(k + 1) * per], q[k * per:(k + 1) * per], seconds, 10000) for k in range(procs)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    rate = sum(d / el for d, el in res)
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:  # noqa: BLE001
+        model = "unknown"
+    return {"value": rate, "unit": "QPs/s", "cores": procs, "kind": "reference",
+            "solver": "qp_solvers.c admm() (the reference's only constrained solver), box +-10 compiled in, "
+                      "ADMM_ITERATIONS 1e4",
+            "sample": f"{len(q)} QPs of the bench batch cycled for {seconds:.0f} s per process, "
+                      f"{procs} forked processes",
+            "cpu_model": model}
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536, help="QPs per GPU")
+    ap.add_argument("--n", type=int, default=16)
+    ap.add_argument("--family", choices=["box", "dense"], default="box")
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-sample", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify statuses after the timed region")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    import qpb
+
+    n, m, B = args.n, 2 * args.n, args.batch
+    # rank r owns QP indices [r*B, (r+1)*B): its own RNG stream
+    H, f, A, b = make_batch(torch, B, n, args.family, args.seed * 1000 + rank, device)
+    sol = qpb.solve(H, f, A, b)  # allocate outputs once
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        qpb.solve(H, f, A, b, out=sol)
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        qpb.solve(H, f, A, b, out=sol)
+        evs[k][1].record(stream)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(e) for a, e in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    st = sol.status.cpu()
+    it = sol.iters.cpu().double()
+    ok_frac = float((st == 0).double().mean())
+    if args.check:
+        assert ok_frac == 1.0, torch.bincount(st.long())
+
+    total_qps = B * world * args.steps
+    value = total_qps / elapsed
+    bpq = bytes_per_qp(n, m)
+    achieved = B * bpq / (kern_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.family == "box":
+        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        S = min(args.cpu_sample, B)
+        cpu = cpu_baseline(H[:S].cpu().numpy(), f[:S].cpu().numpy(), args.cpu_seconds, procs)
+
+    if rank == 0:
+        line = {
+            "metric": "QPs/sec (whole node) at n=16,m=32; % HBM roofline",
+            "value": value,
+            "unit": "QPs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (on-device RNG; conditioned box family, SURVEY.md §8d)",
+            "config": {"workload": f"batched active-set QP solve, n={n}, m={m} (A=[I;-I] dense), "
+                                   f"{B} QPs per GPU (BASELINE configs[1])",
+                       "n": n, "m": m, "batch_per_gpu": B, "global_batch": B * world,
+                       "family": args.family, "parallelism": f"qp-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "gi_dense_kernel<2,true>", "bytes_per_qp": bpq,
+                         "kernel_ms": kern_ms},
+            "cpu_baseline": cpu,
+            "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

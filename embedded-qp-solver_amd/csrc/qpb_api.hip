@@ -1,0 +1,205 @@
+// qpb_api.hip -- the C-ABI of include/qpb.h: argument checking, launches,
+// host-pointer convenience wrappers.  No computation happens here: every
+// solve runs in the HIP kernels (qpb_gi.hip, qpb_ref.hip); there is no CPU
+// fallback -- without a usable HIP device the calls fail with
+// QPB_ERR_NO_DEVICE / QPB_ERR_HIP.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "qpb.h"
+
+extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                    const double *b, double *x, double *lam, uint32_t *active,
+                                    int32_t *status, int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q,
+                                     const double *x0, double *x, int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
+                                         const double *x, double *out, hipStream_t stream);
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+static int hip_fail(hipError_t e, const char *what) {
+  return fail(QPB_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+static int check_device(void) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) return fail(QPB_ERR_NO_DEVICE, "no HIP device available");
+  return 0;
+}
+
+static int check_desc(const qpb_desc *d) {
+  if (!d) return fail(QPB_ERR_INVALID_ARG, "desc is NULL");
+  if (d->batch < 0) return fail(QPB_ERR_INVALID_ARG, "batch < 0");
+  if (d->n < 1 || d->m < 0) return fail(QPB_ERR_INVALID_ARG, "n must be >= 1 and m >= 0");
+  if (d->n > QPB_MAX_N || d->m > QPB_MAX_M)
+    return fail(QPB_ERR_UNSUPPORTED, "n=%d m=%d outside this build's kernels (n<=%d, m<=%d)", d->n, d->m,
+                QPB_MAX_N, QPB_MAX_M);
+  if (d->batch > 0x7fffffffLL * 16) return fail(QPB_ERR_UNSUPPORTED, "batch too large for one launch");
+  return 0;
+}
+
+extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, const double *A,
+                         const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
+                         int32_t *iters, void *stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (d->batch == 0) return 0;
+  if (!H || !f || !x || !status) return fail(QPB_ERR_INVALID_ARG, "H, f, x and status are required");
+  if (d->m > 0 && (!A || !b || !lam || !active))
+    return fail(QPB_ERR_INVALID_ARG, "A, b, lam and active are required when m > 0");
+  rc = check_device();
+  if (rc) return rc;
+  hipError_t e = qpb_launch_gi(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
+  return 0;
+}
+
+// ---- host-pointer wrappers -------------------------------------------------
+struct DevBuf {
+  void *p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+static hipError_t up(DevBuf &b, const void *src, size_t bytes) {
+  if (!src || !bytes) return hipSuccess;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) return e;
+  return hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
+}
+static hipError_t alloc(DevBuf &b, const void *dst, size_t bytes) {
+  if (!dst || !bytes) return hipSuccess;
+  return hipMalloc(&b.p, bytes);
+}
+static hipError_t down(void *dst, const DevBuf &b, size_t bytes) {
+  if (!dst || !bytes) return hipSuccess;
+  return hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost);
+}
+
+#define HIPCHK(expr, what)                  \
+  do {                                      \
+    hipError_t e_ = (expr);                 \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+extern "C" int qpb_solve_host(const qpb_desc *d, const double *H, const double *f, const double *A,
+                              const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
+                              int32_t *iters) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (d->batch == 0) return 0;
+  rc = check_device();
+  if (rc) return rc;
+  const size_t B = (size_t)d->batch, n = d->n, m = d->m, w = (m + 31) / 32;
+  DevBuf dH, df, dA, db, dx, dl, da, ds, di;
+  HIPCHK(up(dH, H, B * n * n * 8), "H");
+  HIPCHK(up(df, f, B * n * 8), "f");
+  HIPCHK(up(dA, m ? A : nullptr, B * m * n * 8), "A");
+  HIPCHK(up(db, m ? b : nullptr, B * m * 8), "b");
+  HIPCHK(alloc(dx, x, B * n * 8), "x");
+  HIPCHK(alloc(dl, m ? lam : nullptr, B * m * 8), "lam");
+  HIPCHK(alloc(da, m ? active : nullptr, B * w * 4), "active");
+  HIPCHK(alloc(ds, status, B * 4), "status");
+  HIPCHK(alloc(di, iters, B * 4), "iters");
+  rc = qpb_solve(d, (double *)dH.p, (double *)df.p, (double *)dA.p, (double *)db.p, (double *)dx.p,
+                 (double *)dl.p, (uint32_t *)da.p, (int32_t *)ds.p, (int32_t *)di.p, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize(), "qpb_solve_host kernel");
+  HIPCHK(down(x, dx, B * n * 8), "x D2H");
+  HIPCHK(down(m ? lam : nullptr, dl, B * m * 8), "lam D2H");
+  HIPCHK(down(m ? active : nullptr, da, B * w * 4), "active D2H");
+  HIPCHK(down(status, ds, B * 4), "status D2H");
+  HIPCHK(down(iters, di, B * 4), "iters D2H");
+  return 0;
+}
+
+static int check_ref(const qpb_ref_desc *d) {
+  if (!d) return fail(QPB_ERR_INVALID_ARG, "desc is NULL");
+  if (d->batch < 0 || d->n < 1 || d->iterations < 0) return fail(QPB_ERR_INVALID_ARG, "bad n/batch/iterations");
+  if (d->mode != QPB_REF_NEWTON && d->mode != QPB_REF_ADMM && d->mode != QPB_REF_GD)
+    return fail(QPB_ERR_INVALID_ARG, "unknown ref mode %d", d->mode);
+  if (d->n > 65535) return fail(QPB_ERR_UNSUPPORTED, "n > 65535 (16-bit dimension field, matrix_type.h:14-17)");
+  return 0;
+}
+
+extern "C" int qpb_ref_solve(const qpb_ref_desc *d, const double *P, const double *q, const double *x0,
+                             double *x, int32_t *iters, void *stream) {
+  int rc = check_ref(d);
+  if (rc) return rc;
+  if (d->batch == 0) return 0;
+  if (!P || !q || !x || (!x0 && d->mode != QPB_REF_ADMM)) return fail(QPB_ERR_INVALID_ARG, "P, q, x0, x required");
+  rc = check_device();
+  if (rc) return rc;
+  hipError_t e = qpb_launch_ref(d, P, q, x0, x, iters, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "qpb_ref_solve launch");
+  return 0;
+}
+
+extern "C" int qpb_ref_solve_host(const qpb_ref_desc *d, const double *P, const double *q, const double *x0,
+                                  double *x, int32_t *iters) {
+  int rc = check_ref(d);
+  if (rc) return rc;
+  if (d->batch == 0) return 0;
+  rc = check_device();
+  if (rc) return rc;
+  const size_t B = (size_t)d->batch, n = d->n;
+  DevBuf dP, dq, dx0, dx, di;
+  HIPCHK(up(dP, P, B * n * n * 8), "P");
+  HIPCHK(up(dq, q, B * n * 8), "q");
+  HIPCHK(up(dx0, x0, B * n * 8), "x0");
+  HIPCHK(alloc(dx, x, B * n * 8), "x");
+  HIPCHK(alloc(di, iters, B * 4), "iters");
+  rc = qpb_ref_solve(d, (double *)dP.p, (double *)dq.p, (double *)dx0.p, (double *)dx.p, (int32_t *)di.p,
+                     nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize(), "qpb_ref_solve_host kernel");
+  HIPCHK(down(x, dx, B * n * 8), "x D2H");
+  HIPCHK(down(iters, di, B * 4), "iters D2H");
+  return 0;
+}
+
+extern "C" int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q, double r, const double *x,
+                           double *out, void *stream) {
+  if (n < 1 || batch < 0 || !P || !q || !x || !out) return fail(QPB_ERR_INVALID_ARG, "bad qpb_qf_eval arguments");
+  if (batch == 0) return 0;
+  int rc = check_device();
+  if (rc) return rc;
+  hipError_t e = qpb_launch_qf_eval(n, batch, P, q, r, x, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "qpb_qf_eval launch");
+  return 0;
+}
+
+extern "C" int qpb_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+extern "C" int qpb_set_device(int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  return 0;
+}
+
+extern "C" int qpb_synchronize(void *stream) {
+  hipError_t e = stream ? hipStreamSynchronize((hipStream_t)stream) : hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "synchronize");
+  return 0;
+}
+
+extern "C" const char *qpb_last_error(void) { return g_err; }
+
+extern "C" const char *qpb_version(void) { return "qpb 0.1 (gfx950)"; }

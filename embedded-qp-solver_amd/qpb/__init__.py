@@ -1,0 +1,202 @@
+"""qpb -- Python host binding of the batched MI355X QP solver (include/qpb.h).
+
+Thin ctypes layer over ``lib/libqpb.so`` (built by ``make -C
+embedded-qp-solver_amd``).  Device memory and streams are PyTorch-ROCm tensors
+and streams; every solve runs in the HIP kernels of the library.  There is no
+CPU fallback: importing this module fails loudly when the library is missing,
+and solving fails when no HIP device is present.
+
+The reference's single-QP C API (qp.h / qp_solvers.h) is the C
+compat layer in include/compat/; this module mirrors the batched C-ABI:
+
+    solve(H, f, A, b)          -> qpb_solve       (active set, m > 0)
+    solve(H, f)                -> qpb_solve, m=0  (test/qp_ref.py:35 semantics)
+    ref_solve(mode, P, q, x0)  -> qpb_ref_solve   (qp_solvers.c replicas)
+    qf_eval(P, q, r, x)        -> qpb_qf_eval     (qp.c:9-27)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import NamedTuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.environ.get("QPB_LIB", os.path.join(PKG_ROOT, "lib", "libqpb.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"qpb: {LIB_PATH} not found -- build it with `make -C {PKG_ROOT}` "
+                      "(there is no CPU fallback)")
+
+_lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+
+# status codes (qpb_status)
+OK, MAX_ITER, NOT_SPD, INFEASIBLE, NUMERICAL = 0, 1, 2, 3, 4
+STATUS_NAMES = {OK: "OK", MAX_ITER: "MAX_ITER", NOT_SPD: "NOT_SPD", INFEASIBLE: "INFEASIBLE", NUMERICAL: "NUMERICAL"}
+# error codes (qpb_error)
+ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_DEVICE = -1, -2, -3, -4
+# reference modes (qpb_ref_mode)
+REF_NEWTON, REF_ADMM, REF_GD = 1, 2, 3
+MAX_N, MAX_M = 16, 32
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("m", ctypes.c_int32), ("batch", ctypes.c_int64),
+                ("max_iter", ctypes.c_int32), ("flags", ctypes.c_int32), ("feas_tol", ctypes.c_double)]
+
+
+class RefDesc(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("mode", ctypes.c_int32), ("batch", ctypes.c_int64),
+                ("iterations", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("box_min", ctypes.c_double), ("box_max", ctypes.c_double)]
+
+
+_vp = ctypes.c_void_p
+_lib.qpb_solve.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 10
+_lib.qpb_solve.restype = ctypes.c_int
+_lib.qpb_solve_host.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 9
+_lib.qpb_solve_host.restype = ctypes.c_int
+_lib.qpb_ref_solve.argtypes = [ctypes.POINTER(RefDesc)] + [_vp] * 6
+_lib.qpb_ref_solve.restype = ctypes.c_int
+_lib.qpb_ref_solve_host.argtypes = [ctypes.POINTER(RefDesc)] + [_vp] * 5
+_lib.qpb_ref_solve_host.restype = ctypes.c_int
+_lib.qpb_qf_eval.argtypes = [ctypes.c_int32, ctypes.c_int64, _vp, _vp, ctypes.c_double, _vp, _vp, _vp]
+_lib.qpb_qf_eval.restype = ctypes.c_int
+_lib.qpb_last_error.restype = ctypes.c_char_p
+_lib.qpb_version.restype = ctypes.c_char_p
+_lib.qpb_device_count.restype = ctypes.c_int
+_lib.qpb_set_device.argtypes = [ctypes.c_int]
+_lib.qpb_synchronize.argtypes = [_vp]
+
+
+class QPBError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        msg = _lib.qpb_last_error().decode(errors="replace")
+        super().__init__(f"{where} failed with {code}: {msg}")
+        self.code = code
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != 0:
+        raise QPBError(rc, where)
+
+
+def lib() -> ctypes.CDLL:
+    return _lib
+
+
+def version() -> str:
+    return _lib.qpb_version().decode()
+
+
+def device_count() -> int:
+    return int(_lib.qpb_device_count())
+
+
+class Solution(NamedTuple):
+    x: object       # (B, n) float64
+    lam: object     # (B, m) float64
+    active: object  # (B, ceil(m/32)) int32 (uint32 bit pattern)
+    status: object  # (B,) int32
+    iters: object   # (B,) int32
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() > 0 else ctypes.c_void_p(0)
+
+
+def _stream_ptr(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def solve(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0, out: Solution | None = None,
+          stream=None) -> Solution:
+    """Batched min 1/2 x^T H x + f^T x s.t. A x <= b on the GPU (torch CUDA float64 tensors).
+
+    H (B,n,n), f (B,n), A (B,m,n), b (B,m).  Asynchronous on ``stream``
+    (default: torch's current stream).  A/b omitted -> unconstrained solve.
+    """
+    import torch
+    if not (H.is_cuda and f.is_cuda):
+        raise ValueError("qpb.solve expects CUDA (HIP) tensors; use solve_host for numpy")
+    B, n = f.shape
+    m = 0 if A is None else A.shape[1]
+    for t in (H, f) + ((A, b) if m else ()):
+        if t.dtype != torch.float64 or not t.is_contiguous():
+            raise ValueError("inputs must be contiguous float64")
+    if H.shape != (B, n, n) or (m and (A.shape != (B, m, n) or b.shape != (B, m))):
+        raise ValueError("shape mismatch")
+    dev = f.device
+    w = (m + 31) // 32
+    if out is None:
+        out = Solution(torch.empty((B, n), dtype=torch.float64, device=dev),
+                       torch.empty((B, m), dtype=torch.float64, device=dev),
+                       torch.empty((B, w), dtype=torch.int32, device=dev),
+                       torch.empty((B,), dtype=torch.int32, device=dev),
+                       torch.empty((B,), dtype=torch.int32, device=dev))
+    d = Desc(n, m, B, max_iter, 0, feas_tol)
+    rc = _lib.qpb_solve(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(A) if m else None, _ptr(b) if m else None,
+                        _ptr(out.x), _ptr(out.lam), _ptr(out.active), _ptr(out.status), _ptr(out.iters),
+                        _stream_ptr(stream))
+    _check(rc, "qpb_solve")
+    return out
+
+
+def solve_raw(desc: Desc, ptrs, stream_ptr) -> int:
+    """Direct C-ABI call with raw device pointers (H, f, A, b, x, lam, active, status, iters)."""
+    return _lib.qpb_solve(ctypes.byref(desc), *[ctypes.c_void_p(p) for p in ptrs], ctypes.c_void_p(stream_ptr))
+
+
+def solve_host(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0) -> Solution:
+    """numpy in / numpy out (qpb_solve_host: H2D, solve, D2H)."""
+    import numpy as np
+    H = np.ascontiguousarray(H, dtype=np.float64)
+    f = np.ascontiguousarray(f, dtype=np.float64)
+    B, n = f.shape
+    m = 0 if A is None else A.shape[1]
+    if m:
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+    w = (m + 31) // 32
+    x = np.zeros((B, n))
+    lam = np.zeros((B, m))
+    act = np.zeros((B, w), dtype=np.uint32)
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    d = Desc(n, m, B, max_iter, 0, feas_tol)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None and a.size else None  # noqa: E731
+    rc = _lib.qpb_solve_host(ctypes.byref(d), p(H), p(f), p(A), p(b), p(x), p(lam), p(act), p(st), p(it))
+    _check(rc, "qpb_solve_host")
+    return Solution(x, lam, act, st, it)
+
+
+def active_mask_to_bool(active, m: int):
+    """(B, words) uint32/int32 bit words -> (B, m) bool (numpy)."""
+    import numpy as np
+    a = np.asarray(active).astype(np.uint32)
+    bits = ((a[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(bool)
+    return bits.reshape(a.shape[0], -1)[:, :m]
+
+
+def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), stream=None):
+    """Reference-semantics batched solvers (qp_solvers.c replicas) on CUDA tensors."""
+    import torch
+    B, n = q.shape
+    x = torch.empty((B, n), dtype=torch.float64, device=q.device)
+    it = torch.empty((B,), dtype=torch.int32, device=q.device)
+    d = RefDesc(n, mode, B, iterations, 0, float(box[0]), float(box[1]))
+    rc = _lib.qpb_ref_solve(ctypes.byref(d), _ptr(P), _ptr(q), _ptr(x0) if x0 is not None else None,
+                            _ptr(x), _ptr(it), _stream_ptr(stream))
+    _check(rc, "qpb_ref_solve")
+    return x, it
+
+
+def qf_eval(P, q, r: float, x, stream=None):
+    import torch
+    B, n = q.shape
+    out = torch.empty((B,), dtype=torch.float64, device=q.device)
+    rc = _lib.qpb_qf_eval(n, B, _ptr(P), _ptr(q), float(r), _ptr(x), _ptr(out), _stream_ptr(stream))
+    _check(rc, "qpb_qf_eval")
+    return out

@@ -1,0 +1,140 @@
+/*
+ * qpb.h -- batched dense QP solver for AMD MI355X (gfx950): the C-ABI.
+ *
+ * Plain C, plain pointers and sizes.  This is the drop-in boundary for the
+ * reference's hot path (YangLingyuan/Embedded-qp-solver):
+ *
+ *   reference (one QP, CPU, fp64)                       replaced by
+ *   --------------------------------------------------  ----------------------
+ *   qp_solvers.h:4-16  gradient_descent_with_line_search qpb_ref_solve(QPB_REF_GD)
+ *                      newton_method_with_line_search    qpb_ref_solve(QPB_REF_NEWTON)
+ *                      admm (box = config.h:29-30)       qpb_ref_solve(QPB_REF_ADMM)
+ *   test/qp_ref.py:35  solve_qp(P, q, G=0, h=0)          qpb_solve(m = 0)
+ *   north_star active-set over (H, f, A, b)              qpb_solve(m > 0)
+ *   (absent from the reference: SURVEY.md §0)
+ *   qp.h:19-24         quadratic_form_eval / _eval_grad  qpb_qf_eval
+ *
+ * The single-QP reference API itself (qp.h, qp_solvers.h, matrix_ops.h,
+ * kmalloc.h, matrix_type.h) is re-exported, layout-compatible, by the compat
+ * headers in include/compat/ on top of these entry points.
+ *
+ * Problem (per QP, fp64):   min 1/2 x^T H x + f^T x   s.t.   A x <= b
+ *   H  n x n row-major, symmetric positive definite (the reference's P,
+ *      qp.h:8-13; only the lower triangle is read)
+ *   f  n        (the reference's q)
+ *   A  m x n row-major, b  m   (a box lb <= x <= ub is A = [I; -I], b = [ub; -lb])
+ * Batched layout: QP k's arrays are contiguous at H + k*n*n, f + k*n,
+ * A + k*m*n, b + k*m (array-of-structures, the reference's row-major
+ * struct _matrix elements, matrix_type.h:20-23, one after another).
+ *
+ * Outputs:
+ *   x       n per QP
+ *   lam     m per QP: Lagrange multipliers, H x + f + A^T lam = 0, lam >= 0
+ *   active  ceil(m/32) uint32 words per QP: bit i set <=> row i in the final
+ *           active set
+ *   status  one int32 per QP (qpb_status); never aborts the batch
+ *   iters   one int32 per QP (active-set iterations), may be NULL
+ *
+ * All array pointers passed to qpb_solve / qpb_ref_solve are DEVICE pointers
+ * (hipMalloc'd or torch CUDA tensors) and the call is asynchronous on
+ * `stream` (a hipStream_t, NULL = default stream).  The *_host variants take
+ * host pointers and synchronise.
+ * Return value: 0 on success, a negative qpb_error on an invalid call.
+ * Thread-safe: no global state besides the per-thread last-error string.
+ */
+#ifndef QPB_H
+#define QPB_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QPB_VERSION_MAJOR 0
+#define QPB_VERSION_MINOR 1
+
+/* limits of this build's kernels (n <= 16: one QP per 16-lane DPP row) */
+#define QPB_MAX_N 16
+#define QPB_MAX_M 32
+
+typedef enum qpb_status {
+	QPB_OK = 0,         /* KKT point found (within feas_tol) */
+	QPB_MAX_ITER = 1,   /* iteration cap reached */
+	QPB_NOT_SPD = 2,    /* Cholesky of H failed (pivot <= 0) */
+	QPB_INFEASIBLE = 3, /* constraints proven infeasible */
+	QPB_NUMERICAL = 4   /* non-finite result */
+} qpb_status;
+
+typedef enum qpb_error {
+	QPB_SUCCESS = 0,
+	QPB_ERR_INVALID_ARG = -1,
+	QPB_ERR_UNSUPPORTED = -2, /* size outside this build's kernels */
+	QPB_ERR_HIP = -3,         /* HIP runtime error (see qpb_last_error) */
+	QPB_ERR_NO_DEVICE = -4
+} qpb_error;
+
+typedef struct qpb_desc {
+	int32_t n;        /* variables, 1..QPB_MAX_N */
+	int32_t m;        /* rows of A x <= b, 0..QPB_MAX_M (0: unconstrained) */
+	int64_t batch;    /* number of QPs */
+	int32_t max_iter; /* <= 0: default 4*(n+m)+8 */
+	int32_t flags;    /* reserved, 0 */
+	double feas_tol;  /* <= 0: default 1e-10 (relative, per row) */
+} qpb_desc;
+
+/* Batched active-set solve (dual Goldfarb-Idnani method, one QP per 16-lane
+ * row of a wavefront).  Device pointers; asynchronous on `stream`. */
+int qpb_solve(const qpb_desc *desc, const double *H, const double *f,
+	      const double *A, const double *b, double *x, double *lam,
+	      uint32_t *active, int32_t *status, int32_t *iters, void *stream);
+
+/* Same with host pointers (allocates device buffers, copies, synchronises). */
+int qpb_solve_host(const qpb_desc *desc, const double *H, const double *f,
+		   const double *A, const double *b, double *x, double *lam,
+		   uint32_t *active, int32_t *status, int32_t *iters);
+
+/* Reference-semantics solvers (qp_solvers.c replicas). */
+typedef enum qpb_ref_mode {
+	QPB_REF_NEWTON = 1, /* qp_solvers.c:103-144 (explicit LU inverse, Armijo quirk) */
+	QPB_REF_ADMM = 2,   /* qp_solvers.c:255-319 (rho = 1, alpha = 1, returns x) */
+	QPB_REF_GD = 3      /* qp_solvers.c:65-101 */
+} qpb_ref_mode;
+
+typedef struct qpb_ref_desc {
+	int32_t n;          /* variables (N_DIM of the reference) */
+	int32_t mode;       /* qpb_ref_mode */
+	int64_t batch;
+	int32_t iterations; /* the reference's `iterations` argument */
+	int32_t flags;      /* reserved, 0 */
+	double box_min;     /* ADMM box (config.h:29-30 ADMM_BOX_CONSTRAINT_MIN/MAX) */
+	double box_max;
+} qpb_ref_desc;
+
+/* P n*n, q n, x0 n per QP (device); writes x n per QP and the iteration
+ * count per QP (may be NULL).  x0 is ignored by ADMM, as in the reference
+ * (qp_solvers.c:256). */
+int qpb_ref_solve(const qpb_ref_desc *desc, const double *P, const double *q,
+		  const double *x0, double *x, int32_t *iters, void *stream);
+
+int qpb_ref_solve_host(const qpb_ref_desc *desc, const double *P,
+		       const double *q, const double *x0, double *x,
+		       int32_t *iters);
+
+/* f(x) = 1/2 x^T P x + q^T x + r per QP (qp.c:9-27), batched, device. */
+int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
+		double r, const double *x, double *out, void *stream);
+
+/* housekeeping */
+int qpb_device_count(void);
+int qpb_set_device(int device);
+int qpb_synchronize(void *stream);
+const char *qpb_last_error(void);
+const char *qpb_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QPB_H */

@@ -1,0 +1,295 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  Nothing here is on the product path; the product is the HIP
+library under embedded-qp-solver_amd/.
+
+CPU restatement (numpy) of the reference behaviour on the hot path:
+
+* glibc ``rand()`` (TYPE_3 additive-feedback generator) -- the reference seeds
+  it with ``srand`` (main.c:11) and draws every input through it
+  (matrix_ops.c:677-681).  Restated so inputs are reproducible without the
+  reference build.
+* the reference input generator: ``random_number`` (matrix_ops.c:677-681),
+  ``matrix_random`` (:683-697, row-major draws), ``matirx_random_pos_def``
+  (:699-734: B random, P = B^T B by the sequential-k ``matrix_mult``
+  (:235-271), then scaled by 1/(max*nrows)), in the P, q, x0 order of
+  main.c:37-39.
+* ``test/qp_ref.py``: reads the wire format (qp_ref.py:8-30, written by
+  test/test.c:108-126) and solves ``solve_qp(P, q, G=0, h=0)`` (qp_ref.py:35),
+  i.e. the unconstrained minimiser x* = -P^{-1} q, printing
+  eval_qp = 1/2 x^T P x + q^T x (qp_ref.py:5-6).  ``qpsolvers`` is absent from
+  the image and unpinned, so it is restated as a dense solve.
+* constrained oracle (north_star's active-set path has NO reference
+  implementation -- SURVEY.md §0/§8c): a primal active-set method
+  (Nocedal & Wright, Numerical Optimization, 2nd ed., Alg. 16.3) for
+  min 1/2 x^T H x + f^T x  s.t.  A x <= b, written independently of the GPU's
+  dual (Goldfarb-Idnani) method, plus a KKT certificate.  Parity for this row
+  is pinned by the certificate, not by a reference output.
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+RAND_MAX = 2147483647
+
+# --------------------------------------------------------------------------
+# glibc rand() restatement (TYPE_3, degree 31, separation 3)
+# --------------------------------------------------------------------------
+
+
+class GlibcRand:
+    """Restatement of glibc's srand/rand (stdlib/random_r.c, TYPE_3).
+
+    r[0] = seed; r[i] = 16807 * r[i-1] mod (2^31-1) for i < 31;
+    r[i] = r[i-31] + r[i-3] (mod 2^32) afterwards; the first 310 outputs of
+    the feedback loop are discarded and rand() returns r[i] >> 1.
+    """
+
+    def __init__(self, seed: int = 1):
+        self.seed(seed)
+
+    def seed(self, seed: int) -> None:
+        seed &= 0xFFFFFFFF
+        if seed >= 0x80000000:
+            seed -= 0x100000000  # stored as int32_t
+        if seed == 0:
+            seed = 1
+        r = [0] * 34
+        r[0] = seed
+        for i in range(1, 31):
+            hi, lo = divmod(r[i - 1], 127773) if r[i - 1] >= 0 else (
+                -((-r[i - 1]) // 127773), -((-r[i - 1]) % 127773))
+            word = 16807 * lo - 2836 * hi
+            if word < 0:
+                word += 2147483647
+            r[i] = word
+        for i in range(31, 34):
+            r[i] = r[i - 31]
+        self._r = [x & 0xFFFFFFFF for x in r]
+        # discard 310 outputs (glibc srandom_r: 10 * rand_deg)
+        for _ in range(310):
+            self._next()
+
+    def _next(self) -> int:
+        r = self._r
+        v = (r[-31] + r[-3]) & 0xFFFFFFFF
+        r.append(v)
+        if len(r) > 64:
+            del r[:-34]
+        return v >> 1
+
+    def rand(self) -> int:
+        return self._next()
+
+    def rand_array(self, count: int) -> np.ndarray:
+        return np.array([self._next() for _ in range(count)], dtype=np.float64)
+
+
+def random_number(rng: GlibcRand, lo: float, hi: float, count: int) -> np.ndarray:
+    """matrix_ops.c:677-681: min + r * (max - min) / RAND_MAX (left-to-right)."""
+    r = rng.rand_array(count)
+    return lo + (r * (hi - lo)) / RAND_MAX
+
+
+def ref_random_pos_def(rng: GlibcRand, n: int, lo: float = -1e3, hi: float = 1e3) -> np.ndarray:
+    """matrix_ops.c:699-734 with the sequential-k matrix_mult of :235-271."""
+    B = random_number(rng, lo, hi, n * n).reshape(n, n)  # matrix_random: row-major
+    acc = np.zeros((n, n))
+    for k in range(n):  # P[i][j] = sum_k B^T[i][k] * B[k][j], k ascending, no FMA
+        acc = acc + np.outer(B[k, :], B[k, :])
+    scale = 1.0 / float(hi * n)
+    return acc * scale
+
+
+def ref_generate(seed: int, count: int, n: int, prange=(-1e3, 1e3), qrange=(-1e3, 1e3),
+                 xrange=(-1e3, 1e3)):
+    """count QPs in main.c:37-39 order (P, q, x0) after srand(seed)."""
+    rng = GlibcRand(seed)
+    P = np.empty((count, n, n))
+    q = np.empty((count, n))
+    x0 = np.empty((count, n))
+    for i in range(count):
+        P[i] = ref_random_pos_def(rng, n, *prange)
+        q[i] = random_number(rng, *qrange, n)
+        x0[i] = random_number(rng, *xrange, n)
+    return P, q, x0
+
+
+# --------------------------------------------------------------------------
+# wire format (test/test.c:108-126 writer, test/qp_ref.py:8-30 reader)
+# --------------------------------------------------------------------------
+
+
+def write_wire(path: str, P: np.ndarray, q: np.ndarray) -> None:
+    """[n as double][P row-major n*n][q n], native-endian fp64 (test.c:110-121)."""
+    n = P.shape[0]
+    with open(path, "wb") as fp:
+        fp.write(struct.pack("d", float(n)))
+        fp.write(np.ascontiguousarray(P, dtype=np.float64).tobytes())
+        fp.write(np.ascontiguousarray(q, dtype=np.float64).reshape(n).tobytes())
+
+
+def read_wire(path: str):
+    """qp_ref.py:8-30: returns (n, P (n,n), q (n,))."""
+    with open(path, "rb") as fp:
+        data = fp.read()
+    vals = np.frombuffer(data, dtype=np.float64)
+    n = int(vals[0])
+    P = vals[1:1 + n * n].reshape(n, n).copy()
+    q = vals[1 + n * n:1 + n * n + n].copy()
+    return n, P, q
+
+
+def eval_qp(P, q, x):
+    """qp_ref.py:5-6 (no constant term)."""
+    return 0.5 * x @ P @ x + q @ x
+
+
+def qp_ref_solve(P, q):
+    """qp_ref.py:35 with G=0, h=0: the constraint 0 <= 0 is vacuous, so the
+    solution is the unconstrained minimiser -P^{-1} q."""
+    return np.linalg.solve(P, -q)
+
+
+# --------------------------------------------------------------------------
+# constrained oracle: primal active set (Nocedal & Wright Alg. 16.3)
+# --------------------------------------------------------------------------
+
+
+@dataclass
+class ASResult:
+    x: np.ndarray
+    lam: np.ndarray
+    active: np.ndarray  # bool (m,)
+    iters: int
+    status: int  # 0 ok, 1 max-iter, 3 infeasible start
+
+
+def _eqp(H, g, Aw):
+    n = H.shape[0]
+    k = Aw.shape[0]
+    if k == 0:
+        return np.linalg.solve(H, -g), np.zeros(0)
+    K = np.zeros((n + k, n + k))
+    K[:n, :n] = H
+    K[:n, n:] = Aw.T
+    K[n:, :n] = Aw
+    rhs = np.concatenate([-g, np.zeros(k)])
+    sol = np.linalg.solve(K, rhs)
+    return sol[:n], sol[n:]
+
+
+def active_set_solve(H, f, A, b, x0=None, max_iter=500, tol=1e-11) -> ASResult:
+    """min 1/2 x^T H x + f^T x  s.t.  A x <= b  (H SPD), from a feasible x0.
+
+    Lagrangian convention: H x + f + A^T lam = 0, lam >= 0,
+    lam_i (b_i - a_i^T x) = 0.
+    """
+    H = np.asarray(H, float)
+    f = np.asarray(f, float)
+    A = np.asarray(A, float).reshape(-1, H.shape[0])
+    b = np.asarray(b, float).reshape(-1)
+    n, m = H.shape[0], A.shape[0]
+    x = np.zeros(n) if x0 is None else np.array(x0, float)
+    scale = 1.0 + np.abs(b)
+    if m and np.any(A @ x - b > 1e-9 * scale):
+        return ASResult(x, np.zeros(m), np.zeros(m, bool), 0, 3)
+    W: list[int] = [i for i in range(m) if abs(A[i] @ x - b[i]) <= 1e-12 * scale[i]]
+    # keep W linearly independent
+    Wi: list[int] = []
+    for i in W:
+        if np.linalg.matrix_rank(A[Wi + [i]]) == len(Wi) + 1:
+            Wi.append(i)
+    W = Wi
+    lam_full = np.zeros(m)
+    for it in range(max_iter):
+        g = H @ x + f
+        p, lam = _eqp(H, g, A[W] if W else np.zeros((0, n)))
+        if np.linalg.norm(p, np.inf) <= tol * (1.0 + np.linalg.norm(x, np.inf)):
+            if len(W) == 0 or lam.min() >= -tol * (1.0 + np.abs(lam).max()):
+                lam_full[:] = 0
+                lam_full[W] = np.maximum(lam, 0.0)
+                act = np.zeros(m, bool)
+                act[W] = True
+                return ASResult(x, lam_full, act, it, 0)
+            j = int(np.argmin(lam))
+            W.pop(j)
+            continue
+        Ap = A @ p if m else np.zeros(0)
+        alpha, block = 1.0, -1
+        for i in range(m):
+            if i in W or Ap[i] <= 1e-14 * np.linalg.norm(A[i]) * np.linalg.norm(p):
+                continue
+            ai = (b[i] - A[i] @ x) / Ap[i]
+            if ai < alpha:
+                alpha, block = max(ai, 0.0), i
+        x = x + alpha * p
+        if block >= 0:
+            W.append(block)
+    act = np.zeros(m, bool)
+    act[W] = True
+    return ASResult(x, lam_full, act, max_iter, 1)
+
+
+def kkt_residuals(H, f, A, b, x, lam):
+    """Batched KKT certificate for A x <= b.  Shapes (B,n,n),(B,n),(B,m,n),(B,m),
+    (B,n),(B,m).  Returns dict of per-QP relative residuals:
+      stat  ||H x + f + A^T lam||_inf / (1 + ||f||_inf + ||H||_inf ||x||_inf)
+      prim  max(0, max_i (a_i x - b_i)) / (1 + ||b||_inf + ||A||_inf ||x||_inf)
+      dual  max(0, -min lam) / (1 + ||lam||_inf)
+      comp  max_i |lam_i (b_i - a_i x)| / ((1 + ||lam||_inf)(1 + ||b|| + ||A|| ||x||))
+    """
+    H, f, A, b, x, lam = (np.asarray(v, float) for v in (H, f, A, b, x, lam))
+    r = np.einsum("bij,bj->bi", H, x) + f + np.einsum("bij,bi->bj", A, lam)
+    xn = np.abs(x).max(axis=1)
+    Hn = np.abs(H).sum(axis=2).max(axis=1)
+    stat = np.abs(r).max(axis=1) / (1.0 + np.abs(f).max(axis=1) + Hn * xn)
+    if A.shape[1] == 0:
+        z = np.zeros(len(x))
+        return {"stat": stat, "prim": z, "dual": z, "comp": z}
+    An = np.abs(A).sum(axis=2).max(axis=1)
+    sc = 1.0 + np.abs(b).max(axis=1) + An * xn
+    slack = b - np.einsum("bij,bj->bi", A, x)
+    prim = np.maximum(0.0, -slack.min(axis=1)) / sc
+    ln = 1.0 + np.abs(lam).max(axis=1)
+    dual = np.maximum(0.0, -lam.min(axis=1)) / ln
+    comp = np.abs(lam * slack).max(axis=1) / (ln * sc)
+    return {"stat": stat, "prim": prim, "dual": dual, "comp": comp}
+
+
+# --------------------------------------------------------------------------
+# synthetic families; numpy RNG, seeded
+# --------------------------------------------------------------------------
+
+
+def family_conditioned(seed: int, count: int, n: int, m: int | None = None, box: float = 25.0,
+                       shift: float = 1.0, kind: str = "box"):
+    """H = B^T B / (1e3 n) + shift*I  (the reference generator's P, matrix_ops.c:699-734,
+    shifted so cond(H) stays <~1e6), f ~ U[-1e3, 1e3] (config.h:19-20).
+
+    kind="box"  : A = [I; -I], b = [ub; -lb], ub = -lb = box   (m = 2n; ADMM's box,
+                  qp_solvers.c:277-280, written as a dense A)
+    kind="dense": A rows ~ N(0,1) normalised, b ~ U(0.1, 1) * box * ||row||... (x=0
+                  strictly feasible).
+    """
+    rs = np.random.default_rng(seed)
+    Bm = rs.uniform(-1e3, 1e3, size=(count, n, n))
+    H = np.einsum("bki,bkj->bij", Bm, Bm) / (1e3 * n) + shift * np.eye(n)
+    f = rs.uniform(-1e3, 1e3, size=(count, n))
+    if kind == "box":
+        m = 2 * n
+        A = np.concatenate([np.broadcast_to(np.eye(n), (count, n, n)),
+                            np.broadcast_to(-np.eye(n), (count, n, n))], axis=1).copy()
+        b = np.full((count, m), float(box))
+    elif kind == "dense":
+        m = m or 2 * n
+        A = rs.standard_normal((count, m, n))
+        A /= np.linalg.norm(A, axis=2, keepdims=True)
+        b = rs.uniform(0.1, 1.0, size=(count, m)) * box
+    else:
+        raise ValueError(kind)
+    return H, f, A, b
