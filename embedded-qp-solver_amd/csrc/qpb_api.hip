@@ -13,6 +13,10 @@
 extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const double *f, const double *A,
                                     const double *b, double *x, double *lam, uint32_t *active,
                                     int32_t *status, int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_sections(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                             const double *b, double *x, double *lam, uint32_t *active,
+                                             int32_t *status, int32_t *iters, unsigned long long *sections,
+                                             hipStream_t stream);
 extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q,
                                      const double *x0, double *x, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
@@ -63,6 +67,20 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
   if (rc) return rc;
   hipError_t e = qpb_launch_gi(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
+  return 0;
+}
+
+extern "C" int qpb_solve_sections(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                  const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
+                                  int32_t *iters, unsigned long long *sections, void *stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (d->batch == 0) return 0;
+  if (d->n != 16 || d->m <= 16 || !sections) return fail(QPB_ERR_UNSUPPORTED, "sections: n=16, 16<m<=32 only");
+  rc = check_device();
+  if (rc) return rc;
+  hipError_t e = qpb_launch_gi_sections(d, H, f, A, b, x, lam, active, status, iters, sections, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "qpb_solve_sections launch");
   return 0;
 }
 

@@ -79,3 +79,53 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 }  // namespace qpb
+
+namespace qpb {
+
+// 1/x and 1/sqrt(x) from the hardware estimates (v_rcp_f64 / v_rsq_f64) plus
+// two Newton steps: full fp64 accuracy (<= 1 ulp), ~6 instructions instead of
+// the IEEE division / sqrt expansions.  Callers guarantee x > 0 finite (or
+// discard the result).
+__device__ __forceinline__ double rcp(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
+  y = __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
+  return y;
+}
+__device__ __forceinline__ double rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
+  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
+  return y;
+}
+
+constexpr double kBig = 1.7976931348623157e308;  // DBL_MAX: the "no candidate" key
+
+// min-reduction key: a finite double whose low 5 mantissa bits carry an index
+// (value perturbed by <= 31 ulp).  v_min_f64 over the 16 lanes then yields the
+// minimum and its index together, 3 instructions per DPP step.
+__device__ __forceinline__ double pack_key(double v, int idx) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  return __builtin_bit_cast(double, (b & ~31ull) | (unsigned long long)idx);
+}
+__device__ __forceinline__ int key_index(double k) {
+  return (int)(__builtin_bit_cast(unsigned long long, k) & 31ull);
+}
+__device__ __forceinline__ double row_min(double v) {
+  v = __builtin_fmin(v, ror<8>(v));
+  v = __builtin_fmin(v, ror<4>(v));
+  v = __builtin_fmin(v, ror<2>(v));
+  v = __builtin_fmin(v, ror<1>(v));
+  return v;
+}
+
+// max of a per-row-uniform int over the 4 rows of the wave, as a wave-uniform
+// (SGPR) value: bounds for skipping dead steps of unrolled loops.
+__device__ __forceinline__ int wave_max4(int v) {
+  const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  const int ab = a > b ? a : b, cd = c > d ? c : d;
+  return ab > cd ? ab : cd;
+}
+
+}  // namespace qpb

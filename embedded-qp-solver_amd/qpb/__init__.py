@@ -200,3 +200,25 @@ def qf_eval(P, q, r: float, x, stream=None):
     rc = _lib.qpb_qf_eval(n, B, _ptr(P), _ptr(q), float(r), _ptr(x), _ptr(out), _stream_ptr(stream))
     _check(rc, "qpb_qf_eval")
     return out
+
+
+_lib.qpb_solve_sections.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 11
+_lib.qpb_solve_sections.restype = ctypes.c_int
+SECTION_NAMES = ["load", "cholesky", "substitution", "init", "select", "exchange", "back_solve", "step",
+                 "add", "drop", "loop_exit", "output"]
+
+
+def solve_sections(H, f, A, b, sections, *, max_iter: int = 0, out: Solution | None = None, stream=None):
+    """Diagnostic build of the n=16, m=32 kernel: accumulates per-section wave
+    cycles into the int64 CUDA tensor ``sections`` (12 entries)."""
+    import torch
+    B, n = f.shape
+    m = A.shape[1]
+    if out is None:
+        out = solve(H, f, A, b, max_iter=max_iter, stream=stream)
+    d = Desc(n, m, B, max_iter, 0, 0.0)
+    rc = _lib.qpb_solve_sections(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(A), _ptr(b), _ptr(out.x), _ptr(out.lam),
+                                 _ptr(out.active), _ptr(out.status), _ptr(out.iters), _ptr(sections),
+                                 _stream_ptr(stream))
+    _check(rc, "qpb_solve_sections")
+    return out

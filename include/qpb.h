@@ -75,12 +75,16 @@ typedef enum qpb_error {
 	QPB_ERR_NO_DEVICE = -4
 } qpb_error;
 
+/* diagnostic flag: every QP k reads the inputs of QP (k mod 64) -- kernel
+ * time without HBM latency (outputs are still written for every k) */
+#define QPB_FLAG_DIAG_L2 1
+
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */
 	int32_t m;        /* rows of A x <= b, 0..QPB_MAX_M (0: unconstrained) */
 	int64_t batch;    /* number of QPs */
 	int32_t max_iter; /* <= 0: default 4*(n+m)+8 */
-	int32_t flags;    /* reserved, 0 */
+	int32_t flags;    /* 0; QPB_FLAG_DIAG_L2 = diagnostic (see below) */
 	double feas_tol;  /* <= 0: default 1e-10 (relative, per row) */
 } qpb_desc;
 
@@ -125,6 +129,15 @@ int qpb_ref_solve_host(const qpb_ref_desc *desc, const double *P,
 /* f(x) = 1/2 x^T P x + q^T x + r per QP (qp.c:9-27), batched, device. */
 int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
 		double r, const double *x, double *out, void *stream);
+
+/* Diagnostic: same solve (n = 16, 16 < m <= 32) by a build of the kernel
+ * with s_memtime stamps; adds each wavefront's cycles per kernel section
+ * (12 counters: load, cholesky, substitution, init, select, exchange,
+ * back-solve, step, add, drop, loop-exit, output) into sections[]. */
+int qpb_solve_sections(const qpb_desc *desc, const double *H, const double *f,
+		       const double *A, const double *b, double *x, double *lam,
+		       uint32_t *active, int32_t *status, int32_t *iters,
+		       unsigned long long *sections, void *stream);
 
 /* housekeeping */
 int qpb_device_count(void);
