@@ -59,6 +59,21 @@ def make_batch(torch, B: int, n: int, family: str, seed: int, device, box: float
     return H.contiguous(), f.contiguous(), A.contiguous(), b.contiguous()
 
 
+def pmc_traffic(n: int, m: int, B: int, family: str):
+    """HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE,
+    WRITE_SIZE; gfx950-corrected, tools/summarize_profile.py) for this exact
+    kernel configuration, from the committed profiles/pmc_traffic.json, or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    c = t.get("config", {})
+    if (c.get("n"), c.get("m"), c.get("batch_per_gpu"), c.get("family")) != (n, m, B, family):
+        return None
+    return {"bytes": t["hbm_bytes_per_launch"], "source": t.get("source", path)}
+
+
 # --------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
     lib_path, P, q, seconds, iters = args
@@ -184,6 +199,7 @@ def main():
     bpq = bytes_per_qp(n, m)
     achieved = B * bpq / (kern_ms * 1e-3) / 1e9
 
+    traffic = pmc_traffic(n, m, B, args.family)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.family == "box":
         procs = args.cpu_procs or min(16, os.cpu_count() or 1)
@@ -209,7 +225,9 @@ def main():
                        "n": n, "m": m, "batch_per_gpu": B, "global_batch": B * world,
                        "family": args.family, "parallelism": f"qp-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic["bytes"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
                          "kernel": "gi_dense_kernel<2,true>", "bytes_per_qp": bpq,
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,

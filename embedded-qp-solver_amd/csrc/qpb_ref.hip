@@ -1,13 +1,308 @@
 // qpb_ref.hip -- reference-semantics kernels and the
 // batched quadratic-form evaluation (qp.c:9-27).
 //
-// Compiled with -ffp-contract=off: the reference's arithmetic (gcc -O2,
-// x86-64, no FMA) rounds every product and sum separately, and these kernels
-// reproduce its operation order.
+// Batched GPU replicas of the reference solvers, operation for operation:
+//   newton_method_with_line_search   qp_solvers.c:103-144
+//   admm                             qp_solvers.c:255-319 (rho = 1, alpha = 1,
+//                                    returns x, x0 ignored)
+//   gradient_descent_with_line_search qp_solvers.c:65-101
+// with the explicit inverse of matrix_invert (partial-pivot LU, matrix_ops.c:
+// 487-536, per-column forward/back substitution :594-625), the Armijo test's
+// f(x + 2 alpha d) quirk (qp_solvers.c:21-35 called from :50-56), matrix_norm's
+// sequential sum of squares (:632-656) and matrix_mult's sequential k-sums
+// (:235-271).  This file is compiled with -ffp-contract=off: the reference
+// (gcc -O2, x86-64, no FMA) rounds every product and every sum, and so do
+// these kernels, in the same order.
+//
+// Layout: one QP per 64-thread workgroup; thread i owns row i (n <= 64).
+// LDS: P, the inverse, two n x n scratch matrices for the per-column solves
+// (thread t keeps its column's vectors in column t: conflict-free) and the
+// n-vectors.
 #include "qpb_common.h"
 #include "qpb.h"
 
 namespace qpb {
+
+constexpr int REF_MAXN = 64;
+constexpr int REF_THREADS = 64;
+
+struct RefShared {
+  double *P, *M, *W, *V;  // n*n each (M: LU then inverse is V)
+  double *x, *g, *d, *t0, *t1, *t2;  // n each
+  double *scal;                       // scalars broadcast by thread 0
+  int *perm;
+};
+
+// prod_i = sum_k A[i][k] * v[k], k ascending (matrix_mult, matrix_ops.c:262-270)
+__device__ __forceinline__ double row_dot(const double *A, const double *v, int i, int n) {
+  double acc = 0.0;
+  for (int k = 0; k < n; ++k) acc += A[i * n + k] * v[k];
+  return acc;
+}
+
+// matrix_scalar_prod (matrix_ops.c:295-297): sequential
+__device__ __forceinline__ double seq_dot(const double *a, const double *b, int n) {
+  double acc = 0.0;
+  for (int k = 0; k < n; ++k) acc += a[k] * b[k];
+  return acc;
+}
+
+// matrix_norm (matrix_ops.c:647-655)
+__device__ __forceinline__ double seq_norm(const double *a, int n) {
+  double acc = 0.0;
+  for (int k = 0; k < n; ++k) {
+    double t = a[k];
+    t *= t;
+    acc += t;
+  }
+  return __builtin_sqrt(acc);
+}
+
+// In-place explicit inverse of S.M (n x n), result in S.V (matrix_invert,
+// matrix_ops.c:551-630).  Thread i: row i in the LU, column i in the solves.
+__device__ void ref_invert(RefShared &S, int n) {
+  const int tid = threadIdx.x;
+  if (tid < n) S.perm[tid] = tid;
+  __syncthreads();
+  bool singular = false;
+  for (int k = 0; k + 1 < n; ++k) {  // matrix_lup_decompose :507
+    if (tid == 0) {                  // matrix_lup_pivot :449-470 (first strict max)
+      double piv = 0.0;
+      int pidx = 0;
+      for (int i = k; i < n; ++i) {
+        double v = S.M[i * n + k];
+        v = v < 0 ? -v : v;
+        if (v > piv) {
+          piv = v;
+          pidx = i;
+        }
+      }
+      S.scal[0] = piv;
+      S.perm[REF_MAXN] = pidx;
+    }
+    __syncthreads();
+    if (S.scal[0] == 0.0) {  // singular: the reference prints and returns (:511-515)
+      singular = true;
+      break;
+    }
+    const int pidx = S.perm[REF_MAXN];
+    if (tid == 0) {  // permutation_swap :434-447
+      const int tmp = S.perm[pidx];
+      S.perm[pidx] = S.perm[k];
+      S.perm[k] = tmp;
+    }
+    if (tid < n) {  // matrix_row_permute :472-485 (thread tid swaps column tid)
+      const double a = S.M[pidx * n + tid], b = S.M[k * n + tid];
+      S.M[pidx * n + tid] = b;
+      S.M[k * n + tid] = a;
+    }
+    __syncthreads();
+    if (tid > k && tid < n) {  // :523-533
+      const int i = tid;
+      double tmp = S.M[i * n + k];
+      tmp /= S.M[k * n + k];
+      S.M[i * n + k] = tmp;
+      for (int j = k + 1; j < n; ++j) {
+        double t = S.M[i * n + j];
+        t -= S.M[i * n + k] * S.M[k * n + j];
+        S.M[i * n + j] = t;
+      }
+    }
+    __syncthreads();
+  }
+  (void)singular;
+  // per-column solves (:594-619): thread i solves for column i; its w/v
+  // vectors are column i of W/V, so V ends up as the inverse (:621-625)
+  if (tid < n) {
+    const int i = tid;
+    for (int nn = 0; nn < n; ++nn) {
+      double t = 0.0;
+      for (int k = 0; k + 1 <= nn; ++k) t += S.M[nn * n + k] * S.W[k * n + i];
+      const double e = (S.perm[nn] == i) ? 1.0 : 0.0;
+      S.W[nn * n + i] = e - t;
+    }
+    for (int nn = n - 1; nn >= 0; --nn) {
+      double t = 0.0;
+      for (int k = nn + 1; k < n; ++k) t += S.M[nn * n + k] * S.V[k * n + i];
+      S.V[nn * n + i] = (S.W[nn * n + i] - t) / S.M[nn * n + nn];
+    }
+  }
+  __syncthreads();
+}
+
+// f(x) = 1/2 x^T (P x) + q^T x + r (quadratic_form_eval, qp.c:9-27); xv in LDS;
+// uses S.t2 as the P x temporary; result broadcast in S.scal[slot].
+__device__ double ref_eval(RefShared &S, const double *q, const double *xv, int n, int slot) {
+  const int tid = threadIdx.x;
+  if (tid < n) S.t2[tid] = row_dot(S.P, xv, tid, n);
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.5 * seq_dot(xv, S.t2, n);
+    a += seq_dot(q, xv, n);
+    a += 0.0;  // r = 0 in every reference call path (main.c:12)
+    S.scal[slot] = a;
+  }
+  __syncthreads();
+  return S.scal[slot];
+}
+
+// grad f(x) = P x + q into out (quadratic_form_eval_grad, qp.c:29-44)
+__device__ void ref_grad(RefShared &S, const double *q, const double *xv, double *out, int n) {
+  const int tid = threadIdx.x;
+  if (tid < n) {
+    const double px = row_dot(S.P, xv, tid, n);
+    out[tid] = px + q[tid];
+  }
+  __syncthreads();
+}
+
+// line_search + armijo (qp_solvers.c:21-63); d in S.d, x in S.x; returns alpha
+__device__ double ref_line_search(RefShared &S, const double *q, int n) {
+  const int tid = threadIdx.x;
+  const double C1 = 0.9, C2 = 1e-4;
+  const double fx = ref_eval(S, q, S.x, n, 1);
+  ref_grad(S, q, S.x, S.t0, n);  // grad_fx
+  double alpha = 1.0;            // ALPHA0_* (:11-12)
+  // The reference loop has no trial cap (:51); alpha *= 0.9 reaches 0 (and
+  // then the Armijo test holds) after ~7000 trials for finite data.  The cap
+  // only stops non-finite data from spinning the GPU forever.
+  for (int trial = 0; trial < 20000; ++trial) {
+    if (tid < n) {
+      const double da = alpha * S.d[tid];  // d_alpha = copy(d); scalar_mult(alpha)
+      S.t1[tid] = da;
+    }
+    __syncthreads();
+    if (tid < n) S.g[tid] = (S.x[tid] + S.t1[tid]) + S.t1[tid];  // lhs_arg = xk + d_alpha, xk = x + d_alpha
+    __syncthreads();
+    const double lhs = ref_eval(S, q, S.g, n, 2);
+    if (tid == 0) S.scal[3] = fx + C2 * seq_dot(S.t0, S.t1, n);
+    __syncthreads();
+    const double rhs = S.scal[3];
+    if (lhs <= rhs) break;
+    alpha *= C1;
+  }
+  return alpha;
+}
+
+__global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long long batch, int iterations,
+                                                          double box_min, double box_max,
+                                                          const double *__restrict__ Pg, const double *__restrict__ qg,
+                                                          const double *__restrict__ x0g, double *__restrict__ xg,
+                                                          int32_t *__restrict__ itg) {
+  extern __shared__ double sm[];
+  const long long g = blockIdx.x;
+  if (g >= batch) return;
+  const int tid = threadIdx.x;
+  RefShared S;
+  const int nn2 = n * n;
+  S.P = sm;
+  S.M = S.P + nn2;
+  S.W = S.M + nn2;
+  S.V = S.W + nn2;
+  S.x = S.V + nn2;
+  S.g = S.x + REF_MAXN;
+  S.d = S.g + REF_MAXN;
+  S.t0 = S.d + REF_MAXN;
+  S.t1 = S.t0 + REF_MAXN;
+  S.t2 = S.t1 + REF_MAXN;
+  double *q = S.t2 + REF_MAXN;
+  double *u = q + REF_MAXN;
+  double *z = u + REF_MAXN;
+  S.scal = z + REF_MAXN;
+  S.perm = reinterpret_cast<int *>(S.scal + 8);
+  const double *Pq = Pg + g * (long long)nn2;
+  for (int e = tid; e < nn2; e += blockDim.x) S.P[e] = Pq[e];
+  if (tid < n) {
+    q[tid] = qg[g * n + tid];
+    S.x[tid] = (mode != QPB_REF_ADMM) ? x0g[g * n + tid] : 0.0;
+  }
+  __syncthreads();
+  int it = 0;
+
+  if (mode == QPB_REF_NEWTON || mode == QPB_REF_GD) {
+    const double MIN_GRAD = 1e-1;  // MIN_GRAD_GRAD / MIN_GRAD_NEWTON (:14-15)
+    if (mode == QPB_REF_NEWTON) {  // hessian_inv = invert(copy(P)) (:115-117)
+      for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = S.P[e];
+      __syncthreads();
+      ref_invert(S, n);
+    }
+    for (; it < iterations; ++it) {
+      ref_grad(S, q, S.x, S.g, n);
+      if (tid == 0) S.scal[0] = seq_norm(S.g, n);
+      __syncthreads();
+      if (MIN_GRAD > S.scal[0]) break;  // :83 / :125
+      if (tid < n) {
+        double dv = (mode == QPB_REF_NEWTON) ? row_dot(S.V, S.g, tid, n) : S.g[tid];  // matrix_mult / copy
+        dv = -1.0 * dv;                                                               // scalar_mult(d, -1)
+        S.d[tid] = dv;
+      }
+      __syncthreads();
+      const double alpha = ref_line_search(S, q, n);
+      if (tid < n) {
+        const double da = alpha * S.d[tid];  // scalar_mult(d, alpha)
+        S.x[tid] = S.x[tid] + da;            // matrix_add(x, x, d)
+      }
+      __syncthreads();
+    }
+  } else {  // ADMM (:255-319)
+    const double rho = 1.0, alpha = 1.0, abstol = 1e-4, restol = 1e-2;
+    if (tid < n) {
+      z[tid] = 0.0;
+      u[tid] = 0.0;
+    }
+    for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = S.P[e];
+    __syncthreads();
+    if (tid < n) S.M[tid * n + tid] = S.M[tid * n + tid] + rho;  // R = P + rho I (:285-291)
+    __syncthreads();
+    ref_invert(S, n);  // R^{-1} in S.V (:292)
+    const double sq = __builtin_sqrt((double)n);
+    for (; it < iterations; ++it) {
+      if (tid < n) {
+        S.t0[tid] = z[tid];  // z_old
+        double y1 = z[tid] - u[tid];  // admm_update_x (:146-159)
+        y1 = rho * y1;
+        y1 = y1 - q[tid];
+        S.t1[tid] = y1;
+      }
+      __syncthreads();
+      if (tid < n) {
+        const double xv = row_dot(S.V, S.t1, tid, n);
+        S.x[tid] = xv;
+        double xh = alpha * xv;  // admm_update_x_hat (:161-174)
+        const double tz = (1.0 - alpha) * z[tid];
+        xh = xh + tz;
+        double tt = xh + u[tid];  // admm_update_z (:176-190): max with lb, then min with ub
+        tt = tt > box_min ? tt : box_min;
+        const double zn = tt > box_max ? box_max : tt;
+        z[tid] = zn;
+        const double du = xh - zn;  // admm_update_u (:192-203)
+        u[tid] = u[tid] + du;
+        S.g[tid] = xv - zn;  // for admm_r_norm
+        double ds = zn - S.t0[tid];
+        ds = -rho * ds;  // admm_s_norm (:219-231)
+        S.d[tid] = ds;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        const double r_norm = seq_norm(S.g, n);
+        const double s_norm = seq_norm(S.d, n);
+        const double norm_x = seq_norm(S.x, n), norm_z = seq_norm(z, n);
+        const double norm_max = norm_x > norm_z ? norm_x : norm_z;
+        const double eps_pri = sq * abstol + restol * norm_max;  // :233-241
+        const double norm_u = seq_norm(u, n);
+        const double eps_dual = sq * abstol + restol * rho * norm_u;  // :243-253
+        S.scal[0] = (r_norm < eps_pri && s_norm < eps_dual) ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      if (S.scal[0] != 0.0) {
+        ++it;
+        break;
+      }
+    }
+  }
+  if (tid < n) xg[g * n + tid] = S.x[tid];
+  if (tid == 0 && itg) itg[g] = it;
+}
 
 // f(x) = 1/2 x^T (P x) + q^T x + r with the reference's order of operations:
 // tmp = matrix_mult(P, x) (sequential k), 0.5 * scalar_prod(x, tmp), + q.x, + r.
@@ -41,7 +336,18 @@ extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P
   return hipGetLastError();
 }
 
-extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *, const double *, const double *, const double *, double *,
-                                     int32_t *, hipStream_t) {
-  return hipErrorNotSupported;  // reference-semantics kernels: next milestone
+extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q, const double *x0,
+                                     double *x, int32_t *iters, hipStream_t stream) {
+  if (d->n > qpb::REF_MAXN) return hipErrorInvalidValue;
+  const int n = d->n;
+  const size_t lds = sizeof(double) * (4 * (size_t)n * n + 10 * qpb::REF_MAXN + 8) + sizeof(int) * (qpb::REF_MAXN + 2);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&qpb::ref_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(qpb::ref_kernel, dim3((unsigned)d->batch), dim3(qpb::REF_THREADS), lds, stream, d->mode, n,
+                     (long long)d->batch, d->iterations, d->box_min, d->box_max, P, q, x0, x, iters);
+  return hipGetLastError();
 }

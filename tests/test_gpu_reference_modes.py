@@ -1,0 +1,108 @@
+"""GPU parity of the reference-semantics kernels (qpb_ref_solve) against the
+compiled reference C (golden fixtures from oracle/_ref, tests/golden/).
+
+The kernels replay qp_solvers.c's Newton (:103-144), ADMM (:255-319) and GD
+(:65-101) with matrix_invert's LU inverse and unfused fp64 in the reference's
+operation order, so the answers should agree to the last bit; the test bar is
+north_star's 1e-6 relative, and the bitwise-equal fraction is checked too.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def qpb():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import qpb as q
+    return q
+
+
+def _run(qpb, mode, P, q, x0, iterations, box=(-1e12, 1e12)):
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()  # noqa: E731
+    x, it = qpb.ref_solve(mode, dev(P), dev(q), dev(x0), iterations=iterations, box=box)
+    torch.cuda.synchronize()
+    return x.cpu().numpy(), it.cpu().numpy()
+
+
+def _rel(x, ref):
+    return np.abs(x - ref).max(axis=1) / np.maximum(1e-300, np.abs(ref).max(axis=1))
+
+
+@pytest.mark.parametrize("n", [4, 16, 32])
+def test_newton_matches_reference_c(qpb, n):
+    g = np.load(os.path.join(GOLDEN, f"ref_n{n}.npz"))
+    x, it = _run(qpb, qpb.REF_NEWTON, g["P"], g["q"], g["x0"], 10)  # HESS_ITERATIONS config.h:37
+    err = _rel(x, g["newton_x"])
+    assert err.max() <= TOL, err
+    assert (it >= 1).all() and (it <= 10).all()
+    assert np.mean(err == 0) >= 0.9  # bit-faithful replay
+
+
+@pytest.mark.parametrize("n,box,key", [(4, 1e12, "admm_x_inactive"), (16, 1e12, "admm_x_inactive"),
+                                       (32, 1e12, "admm_x_inactive"), (4, 1e2, "admm_x_active"),
+                                       (16, 1e2, "admm_x_active"), (32, 1e2, "admm_x_active")])
+def test_admm_matches_reference_c(qpb, n, box, key):
+    g = np.load(os.path.join(GOLDEN, f"ref_n{n}.npz"))
+    x, it = _run(qpb, qpb.REF_ADMM, g["P"], g["q"], g["x0"], 10000, box=(-box, box))
+    err = _rel(x, g[key])
+    assert err.max() <= TOL, err
+    assert np.mean(err == 0) >= 0.9
+
+
+def test_admm_bench_family(qpb):
+    """The bench's conditioned box family with the box +-10 compiled into refC."""
+    g = np.load(os.path.join(GOLDEN, "cond_box_n16.npz"))
+    x, it = _run(qpb, qpb.REF_ADMM, g["H"], g["f"], np.zeros_like(g["f"]), 10000, box=(-10.0, 10.0))
+    err = _rel(x, g["admm_x"])
+    assert err.max() <= TOL
+
+
+@pytest.mark.parametrize("n", [4, 16])
+def test_gd_matches_reference_c(qpb, n):
+    g = np.load(os.path.join(GOLDEN, f"ref_n{n}.npz"))
+    k = g["gd_x"].shape[0]
+    x, it = _run(qpb, qpb.REF_GD, g["P"][:k], g["q"][:k], g["x0"][:k], 10000)  # GRAD_ITERATIONS
+    err = _rel(x, g["gd_x"])
+    assert err.max() <= TOL, err
+
+
+@pytest.mark.parametrize("n", [4, 16])
+def test_matrix_invert_replica(qpb, n):
+    """One Newton step from x0 = 0 with P = I would be trivial; instead check
+    the inverse through Newton on q = -P e_j: x* = e_j exactly when the inverse
+    matches the reference's (fixture `inv` = refC matrix_invert(P))."""
+    g = np.load(os.path.join(GOLDEN, f"ref_n{n}.npz"))
+    P = g["P"]
+    inv = g["inv"]
+    # Newton's first direction is -inv @ grad(x0); with x0 = 0, grad = q, so
+    # d = -inv q; compare via 1 iteration with a huge-q problem where the line
+    # search accepts alpha = 0.9 * ... -> just check d through qf
+    B = P.shape[0]
+    q = np.ones((B, n))
+    x0 = np.zeros((B, n))
+    x, _ = _run(qpb, qpb.REF_NEWTON, P, q, x0, 1)
+    d = -np.einsum("bij,bj->bi", inv, q)
+    # x = alpha * d for the accepted alpha (a power of 0.9)
+    ratio = x / d
+    alpha = ratio[:, 0:1]
+    assert np.allclose(ratio, alpha, rtol=1e-9, atol=0)
+    k = np.log(alpha[:, 0]) / np.log(0.9)
+    assert np.allclose(k, np.round(k), atol=1e-6)
+
+
+def test_qf_eval(qpb):
+    g = np.load(os.path.join(GOLDEN, "ref_n16.npz"))
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()  # noqa: E731
+    out = qpb.qf_eval(dev(g["P"]), dev(g["q"]), 0.0, dev(g["x_exact"]))
+    torch.cuda.synchronize()
+    assert np.allclose(out.cpu().numpy(), g["f_exact"], rtol=1e-9)
