@@ -136,7 +136,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="QPs per GPU")
+    ap.add_argument("--batch", type=int, default=65536, help="QPs per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="total QPs sharded over the GPUs (strong scaling; overrides --batch)")
+    ap.add_argument("--gather", action="store_true",
+                    help="after the timed region, all-gather x/lam/active/status over RCCL and time it")
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--family", choices=["box", "dense"], default="box")
     ap.add_argument("--seed", type=int, default=20261015)
@@ -158,8 +162,13 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     import qpb
+    from qpb.dist import gather_results, max_over_ranks, shard
 
-    n, m, B = args.n, 2 * args.n, args.batch
+    n, m = args.n, 2 * args.n
+    if args.global_batch:
+        start, B = shard(args.global_batch, rank, world)
+    else:
+        start, B = rank * args.batch, args.batch
     # rank r owns QP indices [r*B, (r+1)*B): its own RNG stream
     H, f, A, b = make_batch(torch, B, n, args.family, args.seed * 1000 + rank, device)
     sol = qpb.solve(H, f, A, b)  # allocate outputs once
@@ -183,10 +192,16 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(e) for a, e in evs) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device)
+    gather_ms = None
+    if args.gather and world > 1:  # the trivial result gather of SURVEY.md §8e, outside the timed steps
+        barrier()
+        tg = time.perf_counter()
+        full = gather_results({"x": sol.x, "lam": sol.lam, "active": sol.active, "status": sol.status},
+                              args.global_batch or B * world)
+        barrier()
+        gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, device)
+        del full
 
     st = sol.status.cpu()
     it = sol.iters.cpu().double()
@@ -194,7 +209,8 @@ def main():
     if args.check:
         assert ok_frac == 1.0, torch.bincount(st.long())
 
-    total_qps = B * world * args.steps
+    total_B = args.global_batch or B * world
+    total_qps = total_B * args.steps
     value = total_qps / elapsed
     bpq = bytes_per_qp(n, m)
     achieved = B * bpq / (kern_ms * 1e-3) / 1e9
@@ -216,13 +232,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (on-device RNG; conditioned box family, SURVEY.md §8d)",
             "config": {"workload": f"batched active-set QP solve, n={n}, m={m} (A=[I;-I] dense), "
                                    f"{B} QPs per GPU (BASELINE configs[1])",
-                       "n": n, "m": m, "batch_per_gpu": B, "global_batch": B * world,
+                       "n": n, "m": m, "batch_per_gpu": B, "global_batch": total_B,
                        "family": args.family, "parallelism": f"qp-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -232,6 +248,7 @@ def main():
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
+            "gather_ms": gather_ms,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,0 +1,49 @@
+"""qpb.dist -- multi-GPU sharding of a QP batch.
+
+One process per GPU (torchrun).  Every QP is independent, so the batch is
+split into contiguous index ranges, one per rank, and each rank solves its
+range with no communication.  The only collective is the optional final
+result gather over RCCL/xGMI (backend "nccl" = RCCL on ROCm; "gloo" on CPU
+for tests): x, lam, active words and status of every rank to every rank.
+"""
+from __future__ import annotations
+
+
+def shard(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous [start, start + count) of `total` QPs for `rank`; the first
+    total % world ranks take one extra QP."""
+    if world < 1 or not 0 <= rank < world or total < 0:
+        raise ValueError("bad shard arguments")
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Max of a per-rank scalar (bench timing: the slowest rank defines the step)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_results(local: dict, total: int):
+    """All-gather per-rank result shards (dict of tensors with a leading batch
+    dimension, contiguous shards in rank order) into full-batch tensors on
+    every rank.  Shards may differ in length by one QP (see shard())."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    out = {}
+    for key, t in local.items():
+        counts = [shard(total, r, world)[1] for r in range(world)]
+        maxc = max(counts)
+        pad = torch.zeros((maxc,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad)
+        out[key] = torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
+    return out

@@ -20,7 +20,7 @@
  *
  * Problem (per QP, fp64):   min 1/2 x^T H x + f^T x   s.t.   A x <= b
  *   H  n x n row-major, symmetric positive definite (the reference's P,
- *      qp.h:8-13; only the lower triangle is read)
+ *      qp.h:8-13; must be symmetric -- the kernels read the full matrix)
  *   f  n        (the reference's q)
  *   A  m x n row-major, b  m   (a box lb <= x <= ub is A = [I; -I], b = [ub; -lb])
  * Batched layout: QP k's arrays are contiguous at H + k*n*n, f + k*n,
@@ -131,7 +131,7 @@ int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
 		double r, const double *x, double *out, void *stream);
 
 /* Diagnostic: same solve (n = 16, 16 < m <= 32) by a build of the kernel
- * with s_memtime stamps; adds each wavefront's cycles per kernel section
+ * with s_memrealtime stamps (100 MHz); adds each wavefront's ticks per kernel section
  * (12 counters: load, cholesky, substitution, init, select, exchange,
  * back-solve, step, add, drop, loop-exit, output) into sections[]. */
 int qpb_solve_sections(const qpb_desc *desc, const double *H, const double *f,
