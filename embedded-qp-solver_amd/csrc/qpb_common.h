@@ -73,8 +73,13 @@ __device__ __forceinline__ void row_argmin(double &v, int &i) {
 // instructions execute in issue order, so only the compiler has to be kept
 // from moving LDS accesses across this point; no s_barrier is issued (the
 // waves of a workgroup run different trip counts and must never meet).
+// Materialise v in a VGPR at this point of the program: IR passes sink pure
+// arithmetic towards its uses (past sched_barriers), which in the unrolled
+// factorisation sweeps keeps whole broadcast rows alive across steps.
+__device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
+
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 

@@ -9,10 +9,12 @@
 // (absent from the reference) is the dual active-set method of
 // Goldfarb & Idnani (Math. Prog. 27, 1983), which needs no feasible start:
 //
-//   setup   H = L L^T (Cholesky, row l of H in lane l, left-looking, row k of
-//           L broadcast by DPP row_newbcast); D = A L^{-T}, y = L^{-1} f by
-//           forward substitution (row k of L read from LDS);
-//           slack of the unconstrained minimiser x0 = -H^{-1} f
+//   setup   H = L L^T, D = A L^{-T}, y = L^{-1} f in ONE right-looking sweep:
+//           step k broadcasts pivot row k of the Schur complement (DPP
+//           row_newbcast from lane k); by symmetry it is also column k, so
+//           the same broadcast drives the Schur update of row l (lane l), the
+//           substitution of both D rows of lane l and the lane-parallel y.
+//           Slack of the unconstrained minimiser x0 = -H^{-1} f
 //           (test/qp_ref.py:35's answer): s = b - A x0 = b + D y.
 //   iterate pick the most violated row p (normalised slack, exact row min);
 //           d = -D[p,:] (= J^T n+ in G-I's notation, J = L^{-T} Q, n+ = -a_p),
@@ -24,17 +26,24 @@
 //                         of R;
 //           partial    -> DROP k: delete column k of R, Givens rotations
 //                         restore triangularity (also applied to D).
+//           Row p travels through an LDS exchange row; the active columns are
+//           zeroed and the Householder vector formed IN LDS (one lane-masked
+//           store each), so no per-element selects run on the VALU.
 //   finish  x = -H^{-1} (f + A^T lam) from the final multipliers (KKT
-//           stationarity): the q active rows of A are re-read, two triangular
-//           solves with L kept in LDS.
+//           stationarity): the q active rows of A are re-read, two lane-
+//           parallel triangular solves with L kept in LDS.
 //
 // Data layout per QP (lane l = 0..15 of the QP's 16-lane DPP row):
 //   registers  rows l + 16 r (r < MR) of D, their slacks, 1/||a_row||,
 //              |D row|^2, active flags; multiplier / row of active position l
-//   LDS        L (packed lower triangle, reciprocal diagonal), R (16 x 18
-//              padded rows, zero diagonal + separate diagonal), exchange row,
-//              Givens parameters, lambda scatter buffer.  The R area doubles
-//              as the staging buffer of the coalesced input transposes.
+//   LDS        L (packed rows, true diagonal) + 1/L_kk, R (16 x 18 padded rows,
+//              zero diagonal + separate diagonal), exchange row, Givens
+//              parameters, lambda scatter buffer.  The R area doubles as the
+//              staging buffer of the coalesced input transposes.
+// No branch or select compares the lane id with a compile-time constant:
+// such masks are hoisted by the compiler and end up spilled (SGPR pressure).
+// Values a lane produces for the whole row are captured by same-address LDS
+// stores from all 16 lanes instead.
 #include "qpb_common.h"
 #include "qpb.h"
 
@@ -42,29 +51,27 @@ namespace qpb {
 
 constexpr int NL = 16;  // lanes per QP
 constexpr int QPB = 4;  // QPs per workgroup (one wavefront)
-constexpr int RS = 18;  // R row stride (doubles): conflict-free b64 / b128 row access
+constexpr int RS = 18;  // row stride (doubles) of the input transposes: conflict-free b128
 
-// packed lower triangle of L with even-length rows (16-byte aligned b128
-// reads): row i starts at sum_{j<i} roundup(j+1, 2) = 2u(u+1) (i = 2u) or
-// 2(u+1)^2 (i = 2u+1)
-__host__ __device__ constexpr int lrow(int i) {
-  const int u = i >> 1;
-  return (i & 1) ? 2 * (u + 1) * (u + 1) : 2 * u * (u + 1);
-}
-constexpr int L_SIZE = lrow(NL);  // 144
+// packed lower triangle of L: row i at i(i+1)/2.  Reads may run past a row's
+// end into the next rows (always inside the QP's slot): the solves never use
+// those values.
+__host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
+constexpr int L_SIZE = lrow(NL);  // 136
 
-constexpr int OFF_L = 0;
-constexpr int OFF_R = OFF_L + L_SIZE;     // 144: R, 16 x RS
-constexpr int OFF_XCH = OFF_R + 16 * RS;  // 432: d (16), s_p, |d|^2
-constexpr int OFF_CS = OFF_XCH + 18;      // Givens cosines (16)
-constexpr int OFF_SN = OFF_CS + 16;       // Givens sines (16)
-constexpr int OFF_RDG = OFF_SN + 16;      // diagonal of R (16)
-constexpr int OFF_LAM = OFF_RDG + 16;     // lambda scatter (32)
-constexpr int SLOT = OFF_LAM + 32;        // 530 doubles per QP
+// LDS slot of one QP: 424 doubles = 3,392 B, 13,568 B per wave -> 12 waves
+// per CU (3 per SIMD, matching the 168-VGPR budget)
+constexpr int OFF_L = 0;                  // L (136)
+constexpr int OFF_R = 136;                // R column-major, 16 x 16: R[i][j] at j*16 + i
+constexpr int OFF_XCH = OFF_R + NL * NL;  // 392: exchange row d (16), s_p, |d|^2; Givens
+                                          // cos / sin (16 + 16); y / x capture; lambda scatter
+constexpr int SLOT = OFF_XCH + 32;        // 424
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
+static_assert(SLOT % 2 == 0 && OFF_R % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
+static_assert(NL * RS <= SLOT - OFF_R, "input transposes are staged in R + xch");
 
 // Diagnostic build only (STAMP = true, qpb_solve_sections): s_memrealtime stamps (100 MHz)
-// accumulate each wave's cycles per kernel section; the real kernel has none.
+// accumulate each wave's ticks per kernel section; the real kernel has none.
 constexpr int kSections = 12;
 template <bool ON>
 struct SectionClock {
@@ -96,47 +103,61 @@ struct SectionClock<true> {
   }
 };
 
-// sum_{j<N} x(j) y(j) with 4 independent accumulators: short dependency
-// chains (the kernel is latency-bound at 2-3 waves per SIMD)
+// sum_{j<N} x(j) y(j) with 2 independent accumulators
 template <int N, class FX, class FY>
-__device__ __forceinline__ double dot4(FX &&x, FY &&y, double init = 0.0) {
-  double a0 = init, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+__device__ __forceinline__ double dot2(FX &&x, FY &&y, double init = 0.0) {
+  double a0 = init, a1 = 0.0;
   unroll<N>([&](auto J) {
     constexpr int j = J;
-    if constexpr (j % 4 == 0) a0 = __builtin_fma(x(j), y(j), a0);
-    if constexpr (j % 4 == 1) a1 = __builtin_fma(x(j), y(j), a1);
-    if constexpr (j % 4 == 2) a2 = __builtin_fma(x(j), y(j), a2);
-    if constexpr (j % 4 == 3) a3 = __builtin_fma(x(j), y(j), a3);
+    if constexpr (j % 2 == 0) a0 = __builtin_fma(x(j), y(j), a0);
+    if constexpr (j % 2 == 1) a1 = __builtin_fma(x(j), y(j), a1);
   });
-  return (a0 + a1) + (a2 + a3);
+  return a0 + a1;
 }
 
-template <int MR, bool N16, bool STAMP = false>
-__global__ __launch_bounds__(64, 2) void gi_dense_kernel(
-    const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
+// 16 doubles from LDS (16-byte aligned) as 8 b128 reads
+__device__ __forceinline__ void lds_row16(const double *src, double (&dst)[NL]) {
+#pragma unroll
+  for (int j = 0; j < NL; j += 2) {
+    const double2 v = *reinterpret_cast<const double2 *>(&src[j]);
+    dst[j] = v.x;
+    dst[j + 1] = v.y;
+  }
+}
+
+// MR: rows of D per lane (m <= 16 MR).  N16: n == 16 (coalesced loads).
+// FULL: n == 16 and m == 16 MR (no padding rows: no masking anywhere).
+// One group = the 4 QPs of a wavefront; `grp` its index, `nxt` the group
+// this wave solves next (< 0: none) -- its input lines are prefetched into
+// the caches while this group iterates (persistent launch).
+template <int MR, bool N16, bool FULL, bool STAMP>
+__device__ __forceinline__ void gi_group(
+    double *lds, const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
     uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
-    long long batch, int max_iter, double feas_tol, int flags = 0,
-    unsigned long long *__restrict__ dbg = nullptr) {
-  __shared__ double lds[QPB * SLOT];
+    long long batch, int max_iter, double feas_tol, int flags, unsigned long long *__restrict__ dbg,
+    long long grp, long long nxt) {
+  static_assert(!FULL || N16, "FULL implies n == 16");
   SectionClock<STAMP> clk;
   const int l = threadIdx.x & (NL - 1);
   const int slot = threadIdx.x >> 4;
-  const long long g = (long long)blockIdx.x * QPB + slot;
-  if (g >= batch) return;  // whole 16-lane rows leave together
+  const long long g = grp * QPB + slot;
+  if (g >= batch) return;  // whole 16-lane rows leave together (last group only)
+  if constexpr (FULL) {
+    n = NL;
+    m = NL * MR;
+  }
 
   double *Lp = lds + slot * SLOT + OFF_L;
-  double *R = lds + slot * SLOT + OFF_R;
+  double *R = lds + slot * SLOT + OFF_R;  // column-major
   double *xch = lds + slot * SLOT + OFF_XCH;
-  double *gcs = lds + slot * SLOT + OFF_CS;
-  double *gsn = lds + slot * SLOT + OFF_SN;
-  double *Rdg = lds + slot * SLOT + OFF_RDG;
-  double *lamb = lds + slot * SLOT + OFF_LAM;
+  double *gcs = xch;       // Givens cosines (DROP only)
+  double *gsn = xch + NL;  // Givens sines
 
   // ------------------------------------------------------------------ load
-  // (flags & QPB_FLAG_DIAG_L2: every QP reads the inputs of QP g mod 64 --
+  // (flags & QPB_FLAG_DIAG_L2: every QP reads the inputs of QP g mod 512 --
   // a diagnostic that takes HBM latency out of the kernel time)
-  const long long gi = (flags & 1) ? (g & 63) : g;
+  const long long gi = (flags & 1) ? (g & 511) : g;
   const double *Hq = Hg + gi * (long long)n * n;
   // m == 0: A/b may be NULL -- point the (masked) row loads at H instead
   const double *Aq = m > 0 ? Ag + gi * (long long)m * n : Hq;
@@ -146,7 +167,7 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
   double s[MR], invn[MR], bl[MR], dn[MR];
   bool act[MR];
   bool infeasible_row = false;
-  if (N16) {
+  if constexpr (N16) {
     // Coalesced 16-byte loads: one instruction reads 2 whole rows (256 B) of
     // each of the wave's 4 QPs -- lane l gets row 2t + (l>>3), columns
     // 2(l&7), 2(l&7)+1.  Rows reach their owner lane through a transpose in
@@ -155,36 +176,33 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
     double2 hv[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) hv[t] = *reinterpret_cast<const double2 *>(&Hq[(2 * t + hr) * NL + hc]);
-    double2 av[MR][8];
-#pragma unroll
-    for (int r = 0; r < MR; ++r)
+    // H and the first 16 rows of A in flight together; the next 16 rows are
+    // issued once H has gone through LDS (their staging registers reuse H's)
+    auto load_a = [&](int r, double2 (&av)[8]) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int row = NL * r + 2 * t + hr;
-        av[r][t] = row < m ? *reinterpret_cast<const double2 *>(&Aq[row * NL + hc]) : make_double2(0.0, 0.0);
+        if constexpr (FULL)
+          av[t] = *reinterpret_cast<const double2 *>(&Aq[row * NL + hc]);
+        else
+          av[t] = row < m ? *reinterpret_cast<const double2 *>(&Aq[row * NL + hc]) : make_double2(0.0, 0.0);
       }
-#pragma unroll
-    for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&R[(2 * t + hr) * RS + hc]) = hv[t];
-    wave_lds_sync();
-#pragma unroll
-    for (int j = 0; j < NL; j += 2) {
-      const double2 v = *reinterpret_cast<const double2 *>(&R[l * RS + j]);
-      Lr[j] = v.x;
-      Lr[j + 1] = v.y;
-    }
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
+    };
+    auto transpose = [&](const double2 (&v)[8], double (&dst)[NL]) {
       wave_lds_sync();
 #pragma unroll
-      for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&R[(2 * t + hr) * RS + hc]) = av[r][t];
+      for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&R[(2 * t + hr) * RS + hc]) = v[t];
       wave_lds_sync();
-#pragma unroll
-      for (int j = 0; j < NL; j += 2) {
-        const double2 v = *reinterpret_cast<const double2 *>(&R[l * RS + j]);
-        E[r][j] = v.x;
-        E[r][j + 1] = v.y;
-      }
-    }
+      lds_row16(&R[l * RS], dst);
+    };
+    double2 av[8];
+    load_a(0, av);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads issued up front
+    transpose(hv, Lr);
+    if constexpr (MR > 1) load_a(1, hv);
+    __builtin_amdgcn_sched_barrier(0);
+    transpose(av, E[0]);
+    if constexpr (MR > 1) transpose(hv, E[MR - 1]);
     wave_lds_sync();
   } else {  // padded n < 16: clamped per-lane row loads, identity outside n
     const int lc = l < n ? l : n - 1;
@@ -208,8 +226,8 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
     const int row = l + NL * r;
-    const bool ok = row < m;
-    const double nrm2 = dot4<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
+    const bool ok = FULL || row < m;
+    const double nrm2 = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
     const double bv = bq[ok ? row : 0];
     bl[r] = ok ? bv : 0.0;
     invn[r] = nrm2 > 0.0 ? rsq(nrm2) : 0.0;
@@ -218,65 +236,82 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
     act[r] = false;
   }
   const double fv = fg[gi * n + (l < n ? l : n - 1)];
-  const double fl = (l < n) ? fv : 0.0;
-  double yf[NL];
-  unroll<NL>([&](auto J) { yf[J] = bc<J>(fl); });  // f replicated on every lane
+  const double fl = (N16 || l < n) ? fv : 0.0;
   clk.tick(0);
 
-  // ---- Cholesky H = L L^T (left-looking: step k broadcasts row k of L from
-  // lane k by DPP row_newbcast and finishes column k on every lane)
+  // ---- H = L L^T, D = A L^{-T}, y = L^{-1} f: one right-looking sweep.
+  // Step k: pr = row k of the current Schur complement (lane k's Lr, DPP
+  // broadcast) = column k by symmetry, so L[j][k] = pr[j] / sqrt(akk) and
+  //   row l:  Lr[j] -= c pr[j] (j > k),  c = Lr[k] / akk;   Lr[k] = L[l][k]
+  //   D rows: E[k] /= sqrt(akk), E[j] -= E[k] pr[j] / akk (j > k)
+  //   y:      lane-parallel, f_l -= c f_k;  y_k = f_k / sqrt(akk)
+  // Lanes l < k keep updating dead entries of their row (the upper triangle,
+  // never read); y_k and 1/L_kk are captured by same-address LDS stores.
   bool spd = true;
+  double ya = fl;
   unroll<NL>([&](auto K) {
     constexpr int k = K;
     __builtin_amdgcn_sched_barrier(0);
-    const double a = Lr[k] - dot4<k>([&](int j) { return Lr[j]; }, [&](int j) { return bc<k>(Lr[j]); });
-    const double akk = bc<k>(a);
+    double pr[NL];
+    unroll<NL - k>([&](auto J) { pr[k + J] = bc<k>(Lr[k + J]); });
+    const double akk = pr[k];
     spd = spd && (akk > 0.0);
     const double ik = rsq(akk);
-    // row l keeps L[l][0..l]; the diagonal is stored as its reciprocal
-    Lr[k] = (l > k) ? a * ik : ((l == k) ? ik : 0.0);
-  });
-  // L -> LDS, packed rows (lane l writes row l), kept for the final solves
-  unroll<NL / 2>([&](auto J) {
-    constexpr int j = 2 * J;
-    if (j <= l) *reinterpret_cast<double2 *>(&Lp[lrow(l) + j]) = make_double2(Lr[j], Lr[j + 1]);
-  });
-  wave_lds_sync();
-  clk.tick(1);
-
-  // ---- forward substitutions, row k of L read from LDS (same address on the
-  // QP's 16 lanes: broadcast reads): D = A L^{-T} (rows l, l+16), y = L^{-1} f
-  unroll<NL>([&](auto K) {
-    constexpr int k = K;
-    __builtin_amdgcn_sched_barrier(0);
-    double Lk[k + 2];
-    unroll<(k + 2) / 2>([&](auto J) {
-      const double2 v = *reinterpret_cast<const double2 *>(&Lp[lrow(k) + 2 * J]);
-      Lk[2 * J] = v.x;
-      Lk[2 * J + 1] = v.y;
+    const double ik2 = ik * ik;
+    const double c = Lr[k] * ik2;
+    unroll<NL - 1 - k>([&](auto J) {
+      constexpr int j = k + 1 + J;
+      Lr[j] = __builtin_fma(-c, pr[j], Lr[j]);
     });
-    const double ik = Lk[k];
+    Lr[k] *= ik;
 #pragma unroll
-    for (int r = 0; r < MR; ++r)
-      E[r][k] = (E[r][k] - dot4<k>([&](int j) { return Lk[j]; }, [&](int j) { return E[r][j]; })) * ik;
-    yf[k] = (yf[k] - dot4<k>([&](int j) { return Lk[j]; }, [&](int j) { return yf[j]; })) * ik;
+    for (int r = 0; r < MR; ++r) {
+      const double e = E[r][k];
+      const double e2 = e * ik2;
+      E[r][k] = e * ik;
+      unroll<NL - 1 - k>([&](auto J) {
+        constexpr int j = k + 1 + J;
+        E[r][j] = __builtin_fma(-e2, pr[j], E[r][j]);
+        pin(E[r][j]);
+      });
+    }
+    const double fk = bc<k>(ya);
+    ya = __builtin_fma(-c, fk, ya);
+    xch[k] = fk * ik;  // y_k
   });
+  __builtin_amdgcn_sched_barrier(0);
+  // L -> LDS, packed rows (lane l writes row l), kept for the final solves.
+  // Lane l also writes its dead entries j > l, over the start of later rows:
+  // stores go in descending j, and a row's own entry at such an address has
+  // a smaller j, so it lands last (a wave's DS instructions execute in order).
+  unroll<NL>([&](auto J) {
+    constexpr int j = NL - 1 - J;
+    Lp[lrow(l) + j] = Lr[j];
+    wave_lds_sync();
+  });
+  {
+    double yv[NL];
+    lds_row16(xch, yv);
 #pragma unroll
-  for (int r = 0; r < MR; ++r) {
-    s[r] = dot4<NL>([&](int j) { return E[r][j]; }, [&](int j) { return yf[j]; }, bl[r]);
-    dn[r] = dot4<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
+    for (int r = 0; r < MR; ++r) {
+      s[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return yv[j]; }, bl[r]);
+      dn[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
+    }
   }
+  clk.tick(1);
   clk.tick(2);
 
   // ------------------------------------------------------ active-set loop
-  // R (upper triangular, active columns) lives in LDS with a ZERO diagonal;
-  // the diagonal is kept in Rdg[] (and 1/R[l][l] in a register) so the back
-  // substitution needs no masking.
+  // R (upper triangular, active columns; column j = position j, column-major
+  // so the lane-parallel accesses are contiguous) lives in LDS with a ZERO
+  // diagonal; lane l keeps R[l][l] and its reciprocal in registers, so the
+  // back substitution needs no masking.
 #pragma unroll
-  for (int j = 0; j < RS; j += 2) *reinterpret_cast<double2 *>(&R[l * RS + j]) = make_double2(0.0, 0.0);
+  for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&R[l * NL + j]) = make_double2(0.0, 0.0);
   int q = 0;           // active-set size
   double um = 0.0;     // multiplier of active position l
   int iam = -1;        // constraint index at active position l
+  double rdg = 0.0;    // R[l][l]
   double invRd = 0.0;  // 1 / R[l][l]
   int status;
   bool done;
@@ -293,6 +328,18 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
   int it = 0;
   wave_lds_sync();
   clk.tick(3);
+  // prefetch of the next group's H and A lines (one dword per 128-B line);
+  // the values are only consumed at the end, so the loads retire in the
+  // shadow of this group's iterations
+  uint32_t pf0 = 0, pf1 = 0, pf2 = 0;
+  if (nxt >= 0 && FULL) {
+    const long long gn = nxt * QPB + slot < batch ? nxt * QPB + slot : g;
+    const uint32_t *hp = reinterpret_cast<const uint32_t *>(Hg + gn * (NL * NL)) + l * 32;
+    const uint32_t *ap = reinterpret_cast<const uint32_t *>(Ag + gn * (NL * NL * MR)) + l * 32;
+    pf0 = __builtin_nontemporal_load(hp);
+    pf1 = __builtin_nontemporal_load(ap);
+    pf2 = MR > 1 ? __builtin_nontemporal_load(ap + NL * 32) : 0u;
+  }
 
   while (!done && it < max_iter) {
     ++it;
@@ -318,7 +365,9 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
     clk.tick(4);
     const int qmax = wave_max4(q);  // wave-uniform bound on the active set size
 
-    // ---- d = -D[p,:] and s_p to every lane through the exchange row
+    // ---- row p of D and s_p to every lane through the exchange row; the
+    // active columns are then zeroed in LDS: d2 = D[p, q:] (d = -D[p,:] in
+    // G-I's sign convention; the signs are folded into the formulas below)
     const int owner = p & (NL - 1), prow = p >> 4;
     if (l == owner) {
 #pragma unroll
@@ -331,18 +380,17 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
         }
     }
     wave_lds_sync();
-    double d2[NL];  // -D[p, q:] (zero in the active columns)
-#pragma unroll
-    for (int j = 0; j < NL; j += 2) {
-      const double2 v = *reinterpret_cast<const double2 *>(&xch[j]);
-      d2[j] = (j >= q) ? -v.x : 0.0;
-      d2[j + 1] = (j + 1 >= q) ? -v.y : 0.0;
-    }
+    const double Dpl = xch[l];
+    const double Dpq = xch[q];  // q == 16 reads s_p: only used by an ADD, impossible then
     const double sp = xch[NL];
     const double dd = xch[NL + 1];  // |D[p,:]|^2 (invariant under the column rotations)
-    const double dl = -xch[l];
-    const double dq = (q < NL) ? -xch[q] : 0.0;
-    const double nd2 = dot4<NL>([&](int j) { return d2[j]; }, [&](int j) { return d2[j]; });
+    wave_lds_sync();
+    if (l < q) xch[l] = 0.0;
+    wave_lds_sync();
+    double d2[NL];
+    lds_row16(xch, d2);
+    const double dl = -Dpl;  // d1 component of active position l
+    const double nd2 = dot2<NL>([&](int j) { return d2[j]; }, [&](int j) { return d2[j]; });
     clk.tick(5);
 
     // ---- r = R^{-1} d1: lane-parallel back substitution over the active positions
@@ -351,7 +399,7 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
       double acc = (l < q) ? dl : 0.0;
       unroll<NL>([&](auto JJ) {
         constexpr int j = NL - 1 - JJ;
-        if (j < qmax) acc = __builtin_fma(-R[l * RS + j], bc<j>(acc * invRd), acc);
+        if (j < qmax) acc = __builtin_fma(-R[j * NL + l], bc<j>(acc * invRd), acc);
       });
       rm = acc * invRd;  // r_l (0 for l >= q)
     }
@@ -372,32 +420,38 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
       done = true;
       break;
     }
-    if (t2 < kBig) {  // primal step: slacks s -= t A z,  A z = D[:, q:] d2
+    if (t2 < kBig) {  // primal step: slacks s -= t A z,  A z = -D[:, q:] d2
 #pragma unroll
       for (int r = 0; r < MR; ++r)
-        s[r] = __builtin_fma(-t, dot4<NL>([&](int j) { return E[r][j]; }, [&](int j) { return d2[j]; }), s[r]);
+        s[r] = __builtin_fma(t, dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return d2[j]; }), s[r]);
     }
+#pragma unroll
+    for (int r = 0; r < MR; ++r) pin(s[r]);  // d2 dies here, before the ADD reads v
     um = __builtin_fma(-t, rm, um);
     up += t;
     clk.tick(7);
 
     if (t2 <= t1) {
-      // ---------------- ADD p: Householder on columns q.. of D
+      // ---------------- ADD p: Householder on columns q.. of D.  With
+      // dq = -D[p,q]: alpha = -sign(dq) |d2|, v = d2 + alpha e_q (the negated
+      // G-I vector: same reflection), beta = 1 / (|d2|^2 + alpha D[p,q]).
       const double nrm = __builtin_sqrt(nd2);
-      const double alpha = dq >= 0.0 ? -nrm : nrm;
-      const double beta = rcp(nd2 - alpha * dq);
-#pragma unroll
-      for (int j = 0; j < NL; ++j) d2[j] -= (j == q) ? alpha : 0.0;  // d2 -> Householder vector
+      const double alpha = Dpq <= 0.0 ? -nrm : nrm;
+      const double beta = rcp(__builtin_fma(alpha, Dpq, nd2));
+      if (l == q) xch[q] = Dpq + alpha;
+      wave_lds_sync();
+      double v[NL];
+      lds_row16(xch, v);
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
-        const double w = beta * dot4<NL>([&](int j) { return E[r][j]; }, [&](int j) { return d2[j]; });
+        const double w = beta * dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return v[j]; });
 #pragma unroll
-        for (int j = 0; j < NL; ++j) E[r][j] = __builtin_fma(-w, d2[j], E[r][j]);
+        for (int j = 0; j < NL; ++j) E[r][j] = __builtin_fma(-w, v[j], E[r][j]);
       }
       // new column q of R: d1 strictly above the diagonal, alpha on it
-      R[l * RS + q] = (l < q) ? dl : 0.0;
+      R[q * NL + l] = (l < q) ? dl : 0.0;
       if (l == q) {
-        Rdg[q] = alpha;
+        rdg = alpha;
         invRd = rcp(alpha);
         iam = p;
         um = up;
@@ -427,42 +481,36 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
         um = 0.0;
         iam = -1;
       }
-      // full R (diagonal put back), delete column k (lane l owns column l)
+      // full R (diagonal put back), delete column k (lane l owns column l):
+      // row by row, each read instruction precedes the write that could
+      // overwrite what it reads (in-order DS execution)
       wave_lds_sync();
-      if (l < q) R[l * RS + l] = Rdg[l];
-      wave_lds_sync();
-      double colv[NL];
-#pragma unroll
-      for (int i = 0; i < NL; ++i) {
-        if (i < qmax) {
-          const double nxt = R[i * RS + l + 1];
-          const double cur = R[i * RS + l];
-          colv[i] = (l >= k && l < q - 1) ? nxt : ((l == q - 1) ? 0.0 : cur);
-        }
+      if (l < q) R[l * NL + l] = rdg;
+      const bool shift = l >= k && l < q - 1;
+      for (int i = 0; i < qmax; ++i) {
+        wave_lds_sync();
+        const double nxt = R[((l + 1) & (NL - 1)) * NL + i];
+        wave_lds_sync();
+        if (shift) R[l * NL + i] = nxt;
+        else if (l == q - 1) R[l * NL + i] = 0.0;
       }
-      wave_lds_sync();
-#pragma unroll
-      for (int i = 0; i < NL; ++i)
-        if (i < qmax) R[i * RS + l] = colv[i];
       // Givens rotations restore the upper-triangular R
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
-        const double a = R[j * RS + j], bb = R[(j + 1) * RS + j];
+        const double a = R[j * NL + j], bb = R[j * NL + j + 1];
         const double ir = rsq(__builtin_fma(a, a, bb * bb));
         const double cj = a * ir, sj = bb * ir;
-        const double rj = R[j * RS + l], rj1 = R[(j + 1) * RS + l];
+        const double rj = R[l * NL + j], rj1 = R[l * NL + j + 1];
         wave_lds_sync();
         if (l >= j && l < q - 1) {
-          R[j * RS + l] = __builtin_fma(cj, rj, sj * rj1);
-          R[(j + 1) * RS + l] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
+          R[l * NL + j] = __builtin_fma(cj, rj, sj * rj1);
+          R[l * NL + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
         }
-        if (l == 0) {
-          gcs[j] = cj;
-          gsn[j] = sj;
-        }
+        gcs[j] = cj;  // same value from every lane
+        gsn[j] = sj;
       }
       wave_lds_sync();
-      R[(q - 1) * RS + l] = 0.0;
+      R[l * NL + q - 1] = 0.0;
       unroll<NL - 1>([&](auto JJ) {
         constexpr int j = JJ;
         if (j + 1 < qmax && j >= k && j < q - 1) {
@@ -478,12 +526,10 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
       --q;
       // back to the zero-diagonal form
       wave_lds_sync();
-      const double dg = (l < q) ? R[l * RS + l] : 0.0;
+      const double dg = (l < q) ? R[l * NL + l] : 0.0;
       wave_lds_sync();
-      if (l < q) {
-        Rdg[l] = dg;
-        R[l * RS + l] = 0.0;
-      }
+      if (l < q) R[l * NL + l] = 0.0;
+      rdg = dg;
       invRd = (l < q) ? rcp(dg) : 0.0;
       clk.tick(9);
     }
@@ -494,7 +540,9 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
   // ------------------------------------------------------------- outputs
   // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iact_k} (the active rows of
   // A re-read, one coalesced 128-B row per active position), then L y = g,
-  // L^T x = -y with L from LDS (column sweeps, one broadcast per step).
+  // L^T x = -y, lane-parallel: step k broadcasts the finished component from
+  // lane k; finished lanes keep updating (dead values) and the components are
+  // captured by same-address LDS stores.
   const int qm = wave_max4(q);
   double gl = fl;
   {
@@ -502,29 +550,49 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
     // a zero multiplier), then the sum
     const int ias = iam > 0 ? iam : 0;
     const int lc = l < n ? l : n - 1;
-    double arow[NL];
-    unroll<NL>([&](auto K) {
-      constexpr int kk = K;
-      if (kk < qm) arow[kk] = Aq[bci<kk>(ias) * n + lc];
-    });
-    unroll<NL>([&](auto K) {
-      constexpr int kk = K;
-      if (kk < qm) gl = __builtin_fma(bc<kk>(um), (l < n) ? arow[kk] : 0.0, gl);
+    unroll<2>([&](auto H) {
+      constexpr int k0 = 8 * H;
+      double arow[8];
+      __builtin_amdgcn_sched_barrier(0);
+      unroll<8>([&](auto K) {
+        constexpr int kk = k0 + K;
+        if (kk < qm) arow[K] = Aq[bci<kk>(ias) * n + lc];
+      });
+      unroll<8>([&](auto K) {
+        constexpr int kk = k0 + K;
+        if (kk < qm) gl = __builtin_fma(bc<kk>(um), (N16 || l < n) ? arow[K] : 0.0, gl);
+      });
     });
   }
-  // forward: y_k = g_k / L_kk on lane k, then lanes l > k: g_l -= L[l][k] y_k
-  unroll<NL>([&](auto K) {
-    constexpr int kk = K;
-    const double yk = bc<kk>(gl * Lp[lrow(kk) + kk]);
-    gl = (l == kk) ? yk : ((l > kk) ? __builtin_fma(-Lp[lrow(l) + kk], yk, gl) : gl);
-  });
-  // backward: x_k = y_k / L_kk on lane k, then lanes l < k: y_l -= L[k][l] x_k
-  unroll<NL>([&](auto K) {
-    constexpr int kk = NL - 1 - K;
-    const double xk = bc<kk>(gl * Lp[lrow(kk) + kk]);
-    gl = (l == kk) ? xk : ((l < kk) ? __builtin_fma(-Lp[lrow(kk) + l], xk, gl) : gl);
-  });
-  const double xl = -gl;
+  const double invd = rcp(Lp[lrow(l) + l]);
+  double Lrow[NL];  // row l of L (entries past l are dead)
+#pragma unroll
+  for (int j = 0; j < NL; ++j) Lrow[j] = Lp[lrow(l) + j];
+  wave_lds_sync();
+  {
+    double acc = gl;
+    unroll<NL>([&](auto K) {
+      constexpr int kk = K;
+      const double yk = bc<kk>(acc * invd);
+      acc = __builtin_fma(-Lrow[kk], yk, acc);
+      xch[kk] = yk;
+    });
+  }
+  wave_lds_sync();
+  {
+    double acc = xch[l];
+    wave_lds_sync();
+    unroll<NL>([&](auto K) {
+      constexpr int kk = NL - 1 - K;
+      const double xk = bc<kk>(acc * invd);
+      acc = __builtin_fma(-Lp[lrow(kk) + l], xk, acc);
+      xch[kk] = xk;
+    });
+  }
+  wave_lds_sync();
+  const double xl = -xch[l];
+  double *lamb = xch;  // lambda scatter (32), after x is read
+  wave_lds_sync();
   {
     // a non-finite x on any lane -> NUMERICAL for the QP
     const double bad = row_min((__builtin_fabs(xl) < kInf) ? 0.0 : -1.0);
@@ -538,9 +606,9 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
     const int row = l + NL * r;
-    if (row < m) lamg[g * m + row] = lamb[row];
+    if (FULL || row < m) lamg[g * m + row] = lamb[row];
   }
-  if (l < n) xg[g * n + l] = xl;
+  if (N16 || l < n) xg[g * n + l] = xl;
   const int sh = (threadIdx.x & 63) & ~(NL - 1);
   uint32_t w0 = 0;
 #pragma unroll
@@ -553,8 +621,39 @@ __global__ __launch_bounds__(64, 2) void gi_dense_kernel(
     statg[g] = status;
     if (itg) itg[g] = it;
   }
+  asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
   clk.tick(11);
   clk.flush(dbg);
+}
+
+template <int MR, bool N16, bool FULL, bool STAMP = false, int OCC = 2>
+__global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
+    const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
+    const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
+    uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
+    long long batch, int max_iter, double feas_tol, int flags = 0,
+    unsigned long long *__restrict__ dbg = nullptr) {
+  __shared__ double lds[QPB * SLOT];
+  gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
+                                 flags, dbg, blockIdx.x, -1);
+}
+
+// persistent form: the grid covers the resident waves once; each wave walks
+// the groups grp, grp + gridDim.x, ... and prefetches the next one
+template <int MR, bool N16, bool FULL, int OCC = 2>
+__global__ __launch_bounds__(64, OCC) void gi_dense_persistent(
+    const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
+    const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
+    uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
+    long long batch, int max_iter, double feas_tol, int flags) {
+  __shared__ double lds[QPB * SLOT];
+  const long long ngroups = (batch + QPB - 1) / QPB;
+  for (long long grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const long long nxt = grp + gridDim.x < ngroups ? grp + gridDim.x : -1;
+    gi_group<MR, N16, FULL, false>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
+                                   flags, nullptr, grp, nxt);
+    wave_lds_sync();
+  }
 }
 
 }  // namespace qpb
@@ -566,20 +665,37 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
   const long long blocks = (d->batch + qpb::QPB - 1) / qpb::QPB;
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
-#define QPB_GI_LAUNCH(MR, N16)                                                                                     \
-  hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16>), dim3((unsigned)blocks), dim3(64), 0, stream, H, f, A, b, x, \
-                     lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags)
+#define QPB_GI_LAUNCH(MR, N16, FULL)                                                                               \
+  hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL>), dim3((unsigned)blocks), dim3(64), 0, stream, H, f, A, \
+                     b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags)
   const bool n16 = d->n == 16;
   if (d->m <= 16) {
-    if (n16) QPB_GI_LAUNCH(1, true); else QPB_GI_LAUNCH(1, false);
+    if (n16 && d->m == 16) QPB_GI_LAUNCH(1, true, true);
+    else if (n16) QPB_GI_LAUNCH(1, true, false);
+    else QPB_GI_LAUNCH(1, false, false);
   } else {
-    if (n16) QPB_GI_LAUNCH(2, true); else QPB_GI_LAUNCH(2, false);
+    if (n16 && d->m == 32 && (d->flags & 8)) {  // persistent form
+      int dev = 0, cus = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const long long waves = (long long)cus * 8;  // 2 waves per SIMD
+      const unsigned grid = (unsigned)(blocks < waves ? blocks : waves);
+      hipLaunchKernelGGL((qpb::gi_dense_persistent<2, true, true>), dim3(grid), dim3(64), 0, stream, H, f, A, b, x,
+                         lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags);
+    } else if (n16 && d->m == 32 && (d->flags & 4))  // diagnostic: the 2-waves/SIMD build
+      QPB_GI_LAUNCH(2, true, true);
+    else if (n16 && d->m == 32)  // 168 VGPRs, 13.25 KiB LDS: 3 waves per SIMD
+      hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream,
+                         H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
+                         d->flags);
+    else if (n16) QPB_GI_LAUNCH(2, true, false);
+    else QPB_GI_LAUNCH(2, false, false);
   }
 #undef QPB_GI_LAUNCH
   return hipGetLastError();
 }
 
-// diagnostic: per-section wave cycles of the n=16, 16<m<=32 kernel (sections[12])
+// diagnostic: per-section wave ticks of the n=16, 16<m<=32 kernel (sections[12])
 extern "C" hipError_t qpb_launch_gi_sections(const qpb_desc *d, const double *H, const double *f, const double *A,
                                              const double *b, double *x, double *lam, uint32_t *active,
                                              int32_t *status, int32_t *iters, unsigned long long *sections,
@@ -588,7 +704,8 @@ extern "C" hipError_t qpb_launch_gi_sections(const qpb_desc *d, const double *H,
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
   if (d->n != 16 || d->m <= 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true>), dim3((unsigned)blocks), dim3(64), 0, stream, H, f, A, b,
-                     x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags, sections);
+  hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, false, true>), dim3((unsigned)blocks), dim3(64), 0, stream, H, f,
+                     A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags,
+                     sections);
   return hipGetLastError();
 }

@@ -75,9 +75,14 @@ typedef enum qpb_error {
 	QPB_ERR_NO_DEVICE = -4
 } qpb_error;
 
-/* diagnostic flag: every QP k reads the inputs of QP (k mod 64) -- kernel
+/* diagnostic flag: every QP k reads the inputs of QP (k mod 512) -- kernel
  * time without HBM latency (outputs are still written for every k) */
 #define QPB_FLAG_DIAG_L2 1
+/* diagnostic flag: n = 16, m = 32 solved by the 2-waves-per-SIMD build */
+#define QPB_FLAG_DIAG_OCC2 4
+/* diagnostic flag: n = 16, m = 32 by the persistent launch (grid = resident
+ * waves, each walks several 4-QP groups and prefetches the next one) */
+#define QPB_FLAG_DIAG_PERSISTENT 8
 
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */

@@ -32,10 +32,10 @@ def t_kernel(fn, reps=15):
     return ts[len(ts) // 2]
 
 
-def _diag_args(H, f, A, b, sol):
+def _diag_args(H, f, A, b, sol, flags=1):
     import ctypes
     B, n = f.shape
-    d = qpb.Desc(n, A.shape[1], B, 0, 1, 0.0)  # flags = QPB_FLAG_DIAG_L2
+    d = qpb.Desc(n, A.shape[1], B, 0, flags, 0.0)  # 1 = QPB_FLAG_DIAG_L2, 4 = QPB_FLAG_DIAG_OCC2, 8 = persistent
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     return (ctypes.byref(d), p(H), p(f), p(A), p(b), p(sol.x), p(sol.lam), p(sol.active), p(sol.status),
             p(sol.iters), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
@@ -53,6 +53,13 @@ def main():
         out[f"{fam}_m0_setup_ms"] = t_kernel(lambda: qpb.solve(H, f))
         sol2 = qpb.solve(H, f, A, b)
         out[f"{fam}_l2diag_ms"] = t_kernel(lambda: qpb.lib().qpb_solve(*_diag_args(H, f, A, b, sol2)))
+        out[f"{fam}_occ2_ms"] = t_kernel(lambda: qpb.lib().qpb_solve(*_diag_args(H, f, A, b, sol2, 4)))
+        out[f"{fam}_occ2_l2diag_ms"] = t_kernel(lambda: qpb.lib().qpb_solve(*_diag_args(H, f, A, b, sol2, 5)))
+        out[f"{fam}_persist_ms"] = t_kernel(lambda: qpb.lib().qpb_solve(*_diag_args(H, f, A, b, sol2, 8)))
+        torch.cuda.synchronize()
+        out[f"{fam}_persist_match"] = bool(torch.equal(sol2.x, sol.x) and torch.equal(sol2.active, sol.active))
+        its = sol.iters.view(-1, 4).max(dim=1).values.double()
+        out[f"{fam}_wave_trips_mean"] = float(its.mean())
         for mi in (1, 2, 4, 8, 0):
             out[f"{fam}_maxit{mi or 'def'}_ms"] = t_kernel(lambda: qpb.solve(H, f, A, b, max_iter=mi, out=sol))
     # batch scaling (box)
