@@ -59,7 +59,7 @@ def make_batch(torch, B: int, n: int, family: str, seed: int, device, box: float
     return H.contiguous(), f.contiguous(), A.contiguous(), b.contiguous()
 
 
-def pmc_traffic(n: int, m: int, B: int, family: str):
+def pmc_traffic(n: int, m: int, B: int, family: str, library: str):
     """HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE,
     WRITE_SIZE; gfx950-corrected, tools/summarize_profile.py) for this exact
     kernel configuration, from the committed profiles/pmc_traffic.json, or None."""
@@ -70,6 +70,8 @@ def pmc_traffic(n: int, m: int, B: int, family: str):
         return None
     c = t.get("config", {})
     if (c.get("n"), c.get("m"), c.get("batch_per_gpu"), c.get("family")) != (n, m, B, family):
+        return None
+    if t.get("library") != library:  # measured on another kernel revision
         return None
     return {"bytes": t["hbm_bytes_per_launch"], "source": t.get("source", path)}
 
@@ -125,7 +127,7 @@ def cpu_baseline(H, f, seconds: float, procs: int):
     return {"value": rate, "unit": "QPs/s", "cores": procs, "kind": "reference",
             "solver": "qp_solvers.c admm() (the reference's only constrained solver), box +-10 compiled in, "
                       "ADMM_ITERATIONS 1e4",
-            "sample": f"{len(q)} QPs of the bench batch cycled for {seconds:.0f} s per process, "
+            "sample": f"{len(q)} QPs of the bench family (CPU generator) cycled for {seconds:.0f} s per process, "
                       f"{procs} forked processes",
             "cpu_model": model}
 
@@ -155,6 +157,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPU baseline first: its worker processes are forked, which is only safe
+    # before this process initialises the GPU.  The sample is drawn from the
+    # same family on the CPU generator (same distribution as the GPU batch).
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.family == "box":
+        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        Hc, fc, _, _ = make_batch(torch, args.cpu_sample, args.n, "box", args.seed, torch.device("cpu"))
+        cpu = cpu_baseline(Hc.numpy(), fc.numpy(), args.cpu_seconds, procs)
+        del Hc, fc
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -215,12 +226,7 @@ def main():
     bpq = bytes_per_qp(n, m)
     achieved = B * bpq / (kern_ms * 1e-3) / 1e9
 
-    traffic = pmc_traffic(n, m, B, args.family)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.family == "box":
-        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
-        S = min(args.cpu_sample, B)
-        cpu = cpu_baseline(H[:S].cpu().numpy(), f[:S].cpu().numpy(), args.cpu_seconds, procs)
+    traffic = pmc_traffic(n, m, B, args.family, qpb.version())
 
     if rank == 0:
         line = {
@@ -236,7 +242,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (on-device RNG; conditioned box family, SURVEY.md §8d)",
-            "config": {"workload": f"batched active-set QP solve, n={n}, m={m} (A=[I;-I] dense), "
+            "config": {"workload": f"batched active-set QP solve, n={n}, m={m} "
+                                   f"({'box as dense A=[I;-I]' if args.family == 'box' else 'dense random A'}), "
                                    f"{B} QPs per GPU (BASELINE configs[1])",
                        "n": n, "m": m, "batch_per_gpu": B, "global_batch": total_B,
                        "family": args.family, "parallelism": f"qp-shard x{world}"},
@@ -244,11 +251,12 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": "gi_dense_kernel<2,true>", "bytes_per_qp": bpq,
+                         "kernel": "qpb::gi_dense_kernel<2, true, true, false, 3>", "bytes_per_qp": bpq,
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
             "gather_ms": gather_ms,
+            "library": qpb.version(),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -220,4 +220,6 @@ extern "C" int qpb_synchronize(void *stream) {
 
 extern "C" const char *qpb_last_error(void) { return g_err; }
 
-extern "C" const char *qpb_version(void) { return "qpb 0.1 (gfx950)"; }
+// the hot kernel revision is part of the string: profiles/pmc_traffic.json is
+// only trusted for the revision it was measured on (bench.py)
+extern "C" const char *qpb_version(void) { return "qpb 0.2 (gfx950; gi_dense v4: fused sweep, 3 waves/SIMD)"; }

@@ -124,6 +124,22 @@ __device__ __forceinline__ double row_min(double v) {
   return v;
 }
 
+// sum over the 16 lanes of the row by an xor butterfly (quad_perm 1032,
+// quad_perm 2301, row_half_mirror, row_mirror): at every level the two
+// partners add the same two numbers in swapped order, which IEEE addition
+// makes bitwise equal, so all lanes end with the identical sum.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ double row_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return v;
+}
+
 // max of a per-row-uniform int over the 4 rows of the wave, as a wave-uniform
 // (SGPR) value: bounds for skipping dead steps of unrolled loops.
 __device__ __forceinline__ int wave_max4(int v) {

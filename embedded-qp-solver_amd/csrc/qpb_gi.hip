@@ -148,9 +148,14 @@ __device__ __forceinline__ void gi_group(
     m = NL * MR;
   }
 
-  double *Lp = lds + slot * SLOT + OFF_L;
-  double *R = lds + slot * SLOT + OFF_R;  // column-major
-  double *xch = lds + slot * SLOT + OFF_XCH;
+  // LDS slots in the order 0, 2, 1, 3: ds_read_b64 serves 32 lanes (two QPs)
+  // per cycle, and SLOT = 424 doubles is 16 banks mod 64, so neighbouring
+  // slots would collide on contiguous 16-lane reads; slots 0/2 and 1/3 are
+  // 32 banks apart
+  double *base = lds + (((slot & 1) << 1) | (slot >> 1)) * SLOT;
+  double *Lp = base + OFF_L;
+  double *R = base + OFF_R;  // column-major
+  double *xch = base + OFF_XCH;
   double *gcs = xch;       // Givens cosines (DROP only)
   double *gsn = xch + NL;  // Givens sines
 
@@ -336,9 +341,9 @@ __device__ __forceinline__ void gi_group(
     const long long gn = nxt * QPB + slot < batch ? nxt * QPB + slot : g;
     const uint32_t *hp = reinterpret_cast<const uint32_t *>(Hg + gn * (NL * NL)) + l * 32;
     const uint32_t *ap = reinterpret_cast<const uint32_t *>(Ag + gn * (NL * NL * MR)) + l * 32;
-    pf0 = __builtin_nontemporal_load(hp);
-    pf1 = __builtin_nontemporal_load(ap);
-    pf2 = MR > 1 ? __builtin_nontemporal_load(ap + NL * 32) : 0u;
+    pf0 = *hp;
+    pf1 = *ap;
+    pf2 = MR > 1 ? ap[NL * 32] : 0u;
   }
 
   while (!done && it < max_iter) {
@@ -390,7 +395,7 @@ __device__ __forceinline__ void gi_group(
     double d2[NL];
     lds_row16(xch, d2);
     const double dl = -Dpl;  // d1 component of active position l
-    const double nd2 = dot2<NL>([&](int j) { return d2[j]; }, [&](int j) { return d2[j]; });
+    const double nd2 = row_sum(l >= q ? Dpl * Dpl : 0.0);  // |d2|^2
     clk.tick(5);
 
     // ---- r = R^{-1} d1: lane-parallel back substitution over the active positions
@@ -435,7 +440,7 @@ __device__ __forceinline__ void gi_group(
       // ---------------- ADD p: Householder on columns q.. of D.  With
       // dq = -D[p,q]: alpha = -sign(dq) |d2|, v = d2 + alpha e_q (the negated
       // G-I vector: same reflection), beta = 1 / (|d2|^2 + alpha D[p,q]).
-      const double nrm = __builtin_sqrt(nd2);
+      const double nrm = nd2 * rsq(nd2);  // nd2 > 0 here
       const double alpha = Dpq <= 0.0 ? -nrm : nrm;
       const double beta = rcp(__builtin_fma(alpha, Dpq, nd2));
       if (l == q) xch[q] = Dpq + alpha;
@@ -678,9 +683,9 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
       int dev = 0, cus = 0;
       hipGetDevice(&dev);
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      const long long waves = (long long)cus * 8;  // 2 waves per SIMD
+      const long long waves = (long long)cus * 8;  // 2 waves per SIMD (the group loop costs 70 VGPRs)
       const unsigned grid = (unsigned)(blocks < waves ? blocks : waves);
-      hipLaunchKernelGGL((qpb::gi_dense_persistent<2, true, true>), dim3(grid), dim3(64), 0, stream, H, f, A, b, x,
+      hipLaunchKernelGGL((qpb::gi_dense_persistent<2, true, true, 2>), dim3(grid), dim3(64), 0, stream, H, f, A, b, x,
                          lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags);
     } else if (n16 && d->m == 32 && (d->flags & 4))  // diagnostic: the 2-waves/SIMD build
       QPB_GI_LAUNCH(2, true, true);

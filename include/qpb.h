@@ -53,7 +53,7 @@ extern "C" {
 #endif
 
 #define QPB_VERSION_MAJOR 0
-#define QPB_VERSION_MINOR 1
+#define QPB_VERSION_MINOR 2
 
 /* limits of this build's kernels (n <= 16: one QP per 16-lane DPP row) */
 #define QPB_MAX_N 16

@@ -39,6 +39,7 @@ if "FETCH_SIZE_KiB_per_launch" in res and "WRITE_SIZE_KiB_per_launch" in res:
     res["correction"] = "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section)"
 try:
     res["bench"] = json.loads(open(os.path.join(out_dir, "bench.json")).read().strip().splitlines()[-1])
+    res["library"] = res["bench"].get("library")
 except Exception:  # noqa: BLE001
     pass
 print(json.dumps(res, indent=1))
