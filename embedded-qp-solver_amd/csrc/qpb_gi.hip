@@ -115,6 +115,17 @@ __device__ __forceinline__ double dot2(FX &&x, FY &&y, double init = 0.0) {
   return a0 + a1;
 }
 
+// ... and with 4 (shorter dependency chains in the active-set loop)
+template <int N, class FX, class FY>
+__device__ __forceinline__ double dot4(FX &&x, FY &&y) {
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  unroll<N>([&](auto J) {
+    constexpr int j = J;
+    a[j % 4] = __builtin_fma(x(j), y(j), a[j % 4]);
+  });
+  return (a[0] + a[1]) + (a[2] + a[3]);
+}
+
 // 16 doubles from LDS (16-byte aligned) as 8 b128 reads
 __device__ __forceinline__ void lds_row16(const double *src, double (&dst)[NL]) {
 #pragma unroll
@@ -169,9 +180,14 @@ __device__ __forceinline__ void gi_group(
   const double *bq = m > 0 ? bg + gi * (long long)m : Hq;
   double Lr[NL];  // row l of H, becomes row l of L
   double E[MR][NL];
-  double s[MR], invn[MR], bl[MR], dn[MR];
+  double s[MR], invn[MR], bl[MR], dn[MR], thr[MR];
   bool act[MR];
   bool infeasible_row = false;
+  // b and f with the matrices (same round trip)
+  double bv[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) bv[r] = bq[(FULL || l + NL * r < m) ? l + NL * r : 0];
+  const double fv = fg[gi * n + (l < n ? l : n - 1)];
   if constexpr (N16) {
     // Coalesced 16-byte loads: one instruction reads 2 whole rows (256 B) of
     // each of the wave's 4 QPs -- lane l gets row 2t + (l>>3), columns
@@ -181,8 +197,6 @@ __device__ __forceinline__ void gi_group(
     double2 hv[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) hv[t] = *reinterpret_cast<const double2 *>(&Hq[(2 * t + hr) * NL + hc]);
-    // H and the first 16 rows of A in flight together; the next 16 rows are
-    // issued once H has gone through LDS (their staging registers reuse H's)
     auto load_a = [&](int r, double2 (&av)[8]) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -200,14 +214,24 @@ __device__ __forceinline__ void gi_group(
       wave_lds_sync();
       lds_row16(&R[l * RS], dst);
     };
-    double2 av[8];
-    load_a(0, av);
-    __builtin_amdgcn_sched_barrier(0);  // keep the loads issued up front
+    // all input rows in flight at once (one HBM round trip); instruction
+    // selection sinks loads to their first use, so an empty asm consumes
+    // them right here
+    double2 av[MR][8];
+#pragma unroll
+    for (int r = 0; r < MR; ++r) load_a(r, av[r]);
+#pragma unroll
+    for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(bv[r]));
+    asm volatile("" ::"v"(fv));
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      asm volatile("" ::"v"(hv[t].x), "v"(hv[t].y));
+#pragma unroll
+      for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(av[r][t].x), "v"(av[r][t].y));
+    }
     transpose(hv, Lr);
-    if constexpr (MR > 1) load_a(1, hv);
-    __builtin_amdgcn_sched_barrier(0);
-    transpose(av, E[0]);
-    if constexpr (MR > 1) transpose(hv, E[MR - 1]);
+#pragma unroll
+    for (int r = 0; r < MR; ++r) transpose(av[r], E[r]);
     wave_lds_sync();
   } else {  // padded n < 16: clamped per-lane row loads, identity outside n
     const int lc = l < n ? l : n - 1;
@@ -233,14 +257,14 @@ __device__ __forceinline__ void gi_group(
     const int row = l + NL * r;
     const bool ok = FULL || row < m;
     const double nrm2 = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
-    const double bv = bq[ok ? row : 0];
-    bl[r] = ok ? bv : 0.0;
+    bl[r] = ok ? bv[r] : 0.0;
     invn[r] = nrm2 > 0.0 ? rsq(nrm2) : 0.0;
+    // violation threshold of the normalised slack (-inf: zero row, never selected)
+    thr[r] = nrm2 > 0.0 ? -feas_tol * (1.0 + __builtin_fabs(bl[r]) * invn[r]) : -kInf;
     // a zero row is the constant constraint 0 <= b
     infeasible_row = infeasible_row || (ok && nrm2 == 0.0 && bl[r] < -feas_tol * (1.0 + __builtin_fabs(bl[r])));
     act[r] = false;
   }
-  const double fv = fg[gi * n + (l < n ? l : n - 1)];
   const double fl = (N16 || l < n) ? fv : 0.0;
   clk.tick(0);
 
@@ -354,7 +378,7 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const double v = s[r] * invn[r];
-        const bool viol = !act[r] && invn[r] > 0.0 && v < -feas_tol * (1.0 + __builtin_fabs(bl[r]) * invn[r]);
+        const bool viol = !act[r] && v < thr[r];
         key = viol ? __builtin_fmin(key, pack_key(v, l + NL * r)) : key;
       }
       key = row_min(key);
