@@ -40,23 +40,12 @@ def bytes_per_qp(n: int, m: int) -> int:
     return 8 * (n * n + n + m * n + m) + 8 * (n + m) + 4 * ((m + 31) // 32) + 4
 
 
-def make_batch(torch, B: int, n: int, family: str, seed: int, device, box: float = 10.0):
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    Bm = (torch.rand((B, n, n), generator=g, device=device, dtype=torch.float64) * 2 - 1) * 1e3
-    H = torch.bmm(Bm.transpose(1, 2), Bm) / (1e3 * n) + torch.eye(n, device=device, dtype=torch.float64)
-    del Bm
-    H = 0.5 * (H + H.transpose(1, 2))
-    f = (torch.rand((B, n), generator=g, device=device, dtype=torch.float64) * 2 - 1) * 1e3
-    if family == "box":
-        eye = torch.eye(n, device=device, dtype=torch.float64)
-        A = torch.cat([eye, -eye], 0).expand(B, 2 * n, n).contiguous()
-        b = torch.full((B, 2 * n), box, device=device, dtype=torch.float64)
-    else:
-        A = torch.randn((B, 2 * n, n), generator=g, device=device, dtype=torch.float64)
-        A = A / A.norm(dim=2, keepdim=True)
-        b = (torch.rand((B, 2 * n), generator=g, device=device, dtype=torch.float64) * 0.9 + 0.1) * box
-    return H.contiguous(), f.contiguous(), A.contiguous(), b.contiguous()
+def make_batch(torch, B: int, n: int, family: str, seed: int, device, first: int = 0, box: float = 10.0):
+    """QPs [first, first + B) of the benchmark family, generated on the GPU by
+    qpb_generate (Philox keyed by (seed, QP index): a shard is the same QPs as
+    the matching slice of one big batch)."""
+    import qpb
+    return qpb.generate(n, B, seed, family=family, first=first, shift=1.0, box=box, device=device)
 
 
 def pmc_traffic(n: int, m: int, B: int, family: str, library: str):
@@ -127,7 +116,7 @@ def cpu_baseline(H, f, seconds: float, procs: int):
     return {"value": rate, "unit": "QPs/s", "cores": procs, "kind": "reference",
             "solver": "qp_solvers.c admm() (the reference's only constrained solver), box +-10 compiled in, "
                       "ADMM_ITERATIONS 1e4",
-            "sample": f"{len(q)} QPs of the bench family (CPU generator) cycled for {seconds:.0f} s per process, "
+            "sample": f"the batch's first {len(q)} QPs (restated on the CPU) cycled for {seconds:.0f} s per process, "
                       f"{procs} forked processes",
             "cpu_model": model}
 
@@ -158,13 +147,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baseline first: its worker processes are forked, which is only safe
-    # before this process initialises the GPU.  The sample is drawn from the
-    # same family on the CPU generator (same distribution as the GPU batch).
+    # before this process initialises the GPU.  The sample is the first
+    # cpu_sample QPs of the GPU batch, restated on the CPU (oracle.family_generate).
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.family == "box":
         procs = args.cpu_procs or min(16, os.cpu_count() or 1)
-        Hc, fc, _, _ = make_batch(torch, args.cpu_sample, args.n, "box", args.seed, torch.device("cpu"))
-        cpu = cpu_baseline(Hc.numpy(), fc.numpy(), args.cpu_seconds, procs)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # CPU restatement of qpb_generate: the first QPs of the GPU batch
+        Hc, fc, _, _ = oracle.family_generate(args.n, args.cpu_sample, args.seed, "box")
+        cpu = cpu_baseline(Hc, fc, args.cpu_seconds, procs)
         del Hc, fc
     if world > 1:
         import torch.distributed as dist
@@ -181,7 +172,7 @@ def main():
     else:
         start, B = rank * args.batch, args.batch
     # rank r owns QP indices [r*B, (r+1)*B): its own RNG stream
-    H, f, A, b = make_batch(torch, B, n, args.family, args.seed * 1000 + rank, device)
+    H, f, A, b = make_batch(torch, B, n, args.family, args.seed, device, first=start)
     sol = qpb.solve(H, f, A, b)  # allocate outputs once
     torch.cuda.synchronize()
 
@@ -241,7 +232,8 @@ def main():
             "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (on-device RNG; conditioned box family, SURVEY.md §8d)",
+            "data": f"synthetic: qpb_generate on the GPU (Philox keyed by QP index, seed {args.seed}), "
+                    f"conditioned {args.family} family of SURVEY.md §8d",
             "config": {"workload": f"batched active-set QP solve, n={n}, m={m} "
                                    f"({'box as dense A=[I;-I]' if args.family == 'box' else 'dense random A'}), "
                                    f"{B} QPs per GPU (BASELINE configs[1])",

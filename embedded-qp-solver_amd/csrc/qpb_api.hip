@@ -22,6 +22,13 @@ extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, con
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
                                          const double *x, double *out, hipStream_t stream);
 
+extern "C" hipError_t qpb_launch_ref_generate(int n, long long batch, unsigned long long first, unsigned seed,
+                                              const double *range, double *P, double *q, double *x0,
+                                              hipStream_t stream);
+extern "C" hipError_t qpb_launch_generate(int n, int m, long long batch, unsigned long long first,
+                                          unsigned long long seed, int family, double shift, double box, double *H,
+                                          double *f, double *A, double *b, hipStream_t stream);
+
 static thread_local char g_err[512] = "";
 
 static int fail(int code, const char *fmt, ...) {
@@ -200,6 +207,39 @@ extern "C" int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const doub
   return 0;
 }
 
+extern "C" int qpb_ref_generate(const qpb_ref_gen_desc *d, double *P, double *q, double *x0, void *stream) {
+  if (!d) return fail(QPB_ERR_INVALID_ARG, "desc is NULL");
+  if (d->n < 1 || d->batch < 0) return fail(QPB_ERR_INVALID_ARG, "n must be >= 1 and batch >= 0");
+  if (d->n > 64) return fail(QPB_ERR_UNSUPPORTED, "qpb_ref_generate: n=%d > 64", d->n);
+  if (d->batch > 0x7fffffffLL) return fail(QPB_ERR_UNSUPPORTED, "batch too large for one launch");
+  if (d->batch > 0 && (!P || !q || !x0)) return fail(QPB_ERR_INVALID_ARG, "NULL output pointer");
+  int rc = check_device();
+  if (rc) return rc;
+  const double range[6] = {d->p_min, d->p_max, d->q_min, d->q_max, d->x_min, d->x_max};
+  hipError_t e = qpb_launch_ref_generate(d->n, d->batch, d->first, d->seed, range, P, q, x0, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "qpb_ref_generate launch");
+  return 0;
+}
+
+extern "C" int qpb_generate(const qpb_gen_desc *d, double *H, double *f, double *A, double *b, void *stream) {
+  if (!d) return fail(QPB_ERR_INVALID_ARG, "desc is NULL");
+  if (d->n < 1 || d->m < 1 || d->batch < 0) return fail(QPB_ERR_INVALID_ARG, "n, m must be >= 1 and batch >= 0");
+  if (d->family != QPB_FAMILY_BOX && d->family != QPB_FAMILY_DENSE)
+    return fail(QPB_ERR_INVALID_ARG, "unknown family %d", d->family);
+  if (d->family == QPB_FAMILY_BOX && d->m != 2 * d->n)
+    return fail(QPB_ERR_INVALID_ARG, "the box family has m = 2n (got n=%d m=%d)", d->n, d->m);
+  if (d->n > 128) return fail(QPB_ERR_UNSUPPORTED, "qpb_generate: n=%d > 128", d->n);
+  if (d->n > 16 && d->m < d->n) return fail(QPB_ERR_UNSUPPORTED, "qpb_generate: n > 16 needs m >= n");
+  if (d->batch > 0x7fffffffLL) return fail(QPB_ERR_UNSUPPORTED, "batch too large for one launch");
+  if (d->batch > 0 && (!H || !f || !A || !b)) return fail(QPB_ERR_INVALID_ARG, "NULL output pointer");
+  int rc = check_device();
+  if (rc) return rc;
+  hipError_t e = qpb_launch_generate(d->n, d->m, d->batch, d->first, d->seed, d->family, d->shift, d->box, H, f, A,
+                                     b, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "qpb_generate launch");
+  return 0;
+}
+
 extern "C" int qpb_device_count(void) {
   int c = 0;
   if (hipGetDeviceCount(&c) != hipSuccess) return 0;
@@ -222,4 +262,4 @@ extern "C" const char *qpb_last_error(void) { return g_err; }
 
 // the hot kernel revision is part of the string: profiles/pmc_traffic.json is
 // only trusted for the revision it was measured on (bench.py)
-extern "C" const char *qpb_version(void) { return "qpb 0.2 (gfx950; gi_dense v4: fused sweep, 3 waves/SIMD)"; }
+extern "C" const char *qpb_version(void) { return "qpb 0.2 (gfx950; gi_dense v5: fused sweep, one-trip loads, 3 waves/SIMD)"; }

@@ -62,7 +62,7 @@ constexpr int L_SIZE = lrow(NL);  // 136
 // LDS slot of one QP: 424 doubles = 3,392 B, 13,568 B per wave -> 12 waves
 // per CU (3 per SIMD, matching the 168-VGPR budget)
 constexpr int OFF_L = 0;                  // L (136)
-constexpr int OFF_R = 136;                // R column-major, 16 x 16: R[i][j] at j*16 + i
+constexpr int OFF_R = L_SIZE;             // R column-major, 16 x 16: R[i][j] at j*16 + i
 constexpr int OFF_XCH = OFF_R + NL * NL;  // 392: exchange row d (16), s_p, |d|^2; Givens
                                           // cos / sin (16 + 16); y / x capture; lambda scatter
 constexpr int SLOT = OFF_XCH + 32;        // 424
@@ -705,8 +705,8 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
   } else {
     if (n16 && d->m == 32 && (d->flags & 8)) {  // persistent form
       int dev = 0, cus = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       const long long waves = (long long)cus * 8;  // 2 waves per SIMD (the group loop costs 70 VGPRs)
       const unsigned grid = (unsigned)(blocks < waves ? blocks : waves);
       hipLaunchKernelGGL((qpb::gi_dense_persistent<2, true, true, 2>), dim3(grid), dim3(64), 0, stream, H, f, A, b, x,

@@ -13,6 +13,8 @@ compat layer in include/compat/; this module mirrors the batched C-ABI:
     solve(H, f)                -> qpb_solve, m=0  (test/qp_ref.py:35 semantics)
     ref_solve(mode, P, q, x0)  -> qpb_ref_solve   (qp_solvers.c replicas)
     qf_eval(P, q, r, x)        -> qpb_qf_eval     (qp.c:9-27)
+    ref_generate(n, B, seed)   -> qpb_ref_generate (the reference generator, bit for bit)
+    generate(n, B, seed)       -> qpb_generate     (Philox benchmark families)
 """
 from __future__ import annotations
 
@@ -222,3 +224,57 @@ def solve_sections(H, f, A, b, sections, *, max_iter: int = 0, out: Solution | N
                                  _stream_ptr(stream))
     _check(rc, "qpb_solve_sections")
     return out
+
+
+# ------------------------------------------------------------------ generators
+class RefGenDesc(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("seed", ctypes.c_uint32), ("batch", ctypes.c_int64),
+                ("first", ctypes.c_uint64), ("p_min", ctypes.c_double), ("p_max", ctypes.c_double),
+                ("q_min", ctypes.c_double), ("q_max", ctypes.c_double),
+                ("x_min", ctypes.c_double), ("x_max", ctypes.c_double)]
+
+
+class GenDesc(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("m", ctypes.c_int32), ("batch", ctypes.c_int64),
+                ("first", ctypes.c_uint64), ("seed", ctypes.c_uint64), ("family", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("shift", ctypes.c_double), ("box", ctypes.c_double)]
+
+
+FAMILY_BOX, FAMILY_DENSE = 0, 1
+FAMILIES = {"box": FAMILY_BOX, "dense": FAMILY_DENSE}
+_lib.qpb_ref_generate.argtypes = [ctypes.POINTER(RefGenDesc), _vp, _vp, _vp, _vp]
+_lib.qpb_ref_generate.restype = ctypes.c_int
+_lib.qpb_generate.argtypes = [ctypes.POINTER(GenDesc), _vp, _vp, _vp, _vp, _vp]
+_lib.qpb_generate.restype = ctypes.c_int
+
+
+def ref_generate(n: int, batch: int, seed: int, *, first: int = 0, p_range=(-1e3, 1e3), q_range=(-1e3, 1e3),
+                 x_range=(-1e3, 1e3), device=None, stream=None):
+    """The reference generator (srand(seed); main.c:37-39 order) on the GPU,
+    QPs [first, first + batch): (P (B,n,n), q (B,n), x0 (B,n)) CUDA tensors."""
+    import torch
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    P = torch.empty((batch, n, n), dtype=torch.float64, device=dev)
+    q = torch.empty((batch, n), dtype=torch.float64, device=dev)
+    x0 = torch.empty((batch, n), dtype=torch.float64, device=dev)
+    d = RefGenDesc(n, seed & 0xFFFFFFFF, batch, first, *p_range, *q_range, *x_range)
+    _check(_lib.qpb_ref_generate(ctypes.byref(d), _ptr(P), _ptr(q), _ptr(x0), _stream_ptr(stream)),
+           "qpb_ref_generate")
+    return P, q, x0
+
+
+def generate(n: int, batch: int, seed: int, *, family: str = "box", m: int | None = None, first: int = 0,
+             shift: float = 1.0, box: float = 10.0, device=None, stream=None):
+    """Benchmark-family QPs from the counter-based generator (qpb_generate):
+    (H, f, A, b) CUDA tensors; QP first + k is the same for any launch."""
+    import torch
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    m = 2 * n if m is None else m
+    H = torch.empty((batch, n, n), dtype=torch.float64, device=dev)
+    f = torch.empty((batch, n), dtype=torch.float64, device=dev)
+    A = torch.empty((batch, m, n), dtype=torch.float64, device=dev)
+    b = torch.empty((batch, m), dtype=torch.float64, device=dev)
+    d = GenDesc(n, m, batch, first, seed, FAMILIES[family], 0, shift, box)
+    _check(_lib.qpb_generate(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(A), _ptr(b), _stream_ptr(stream)),
+           "qpb_generate")
+    return H, f, A, b

@@ -144,6 +144,50 @@ int qpb_solve_sections(const qpb_desc *desc, const double *H, const double *f,
 		       uint32_t *active, int32_t *status, int32_t *iters,
 		       unsigned long long *sections, void *stream);
 
+/* ------------------------------------------------------------------------
+ * On-device input generators.
+ *
+ * qpb_ref_generate: the reference's generator bit for bit -- srand(seed),
+ * then per QP P = matirx_random_pos_def (matrix_ops.c:699-734), q, x0 =
+ * matrix_random (main.c:37-39 order), glibc TYPE_3 rand().  QPs
+ * [first, first + batch) of that sequence (each QP jumps ahead to its own
+ * offset), so any shard equals the same QPs of one sequential run.
+ * P n*n, q n, x0 n per QP, device pointers.  1 <= n <= 64.              */
+typedef struct qpb_ref_gen_desc {
+	int32_t n;      /* N_DIM */
+	uint32_t seed;  /* srand() argument */
+	int64_t batch;
+	uint64_t first; /* index of the first QP in the sequence */
+	double p_min, p_max; /* random_pos_def range (main.c:37: -1e3, 1e3) */
+	double q_min, q_max; /* q range (main.c:38) */
+	double x_min, x_max; /* x0 range (main.c:39) */
+} qpb_ref_gen_desc;
+
+int qpb_ref_generate(const qpb_ref_gen_desc *desc, double *P, double *q, double *x0, void *stream);
+
+/* qpb_generate: the benchmark families of SURVEY.md §8d from a counter-based
+ * Philox4x32-10 stream keyed by (seed, QP index): QP first + k of any launch
+ * is the same QP.  H = B^T B / (1e3 n) + shift I with B ~ U[-1e3, 1e3]^{n x n}
+ * (product on the fp64 matrix cores), f ~ U[-1e3, 1e3];
+ *   QPB_FAMILY_BOX:   A = [I; -I] (m = 2n), b = box
+ *   QPB_FAMILY_DENSE: rows of A ~ N(0, I) normalised, b ~ U[0.1, 1) box
+ * Device pointers H n*n, f n, A m*n, b m per QP.  1 <= n <= 128; for
+ * n > 16, m >= n (B is staged in A's rows).                             */
+typedef enum qpb_family { QPB_FAMILY_BOX = 0, QPB_FAMILY_DENSE = 1 } qpb_family;
+
+typedef struct qpb_gen_desc {
+	int32_t n, m;
+	int64_t batch;
+	uint64_t first; /* QP index of the first QP generated */
+	uint64_t seed;
+	int32_t family; /* qpb_family */
+	int32_t flags;  /* reserved, 0 */
+	double shift;   /* added to H's diagonal (0: the heavy-tailed "ref" family) */
+	double box;     /* box half-width / b scale */
+} qpb_gen_desc;
+
+int qpb_generate(const qpb_gen_desc *desc, double *H, double *f, double *A, double *b, void *stream);
+
 /* housekeeping */
 int qpb_device_count(void);
 int qpb_set_device(int device);

@@ -293,3 +293,146 @@ def family_conditioned(seed: int, count: int, n: int, m: int | None = None, box:
     else:
         raise ValueError(kind)
     return H, f, A, b
+
+
+# --------------------------------------------------------------------------
+# on-device generators (csrc/qpb_gen.hip), restated for the parity tests
+# --------------------------------------------------------------------------
+
+_M32 = 0xFFFFFFFF
+_GDEG = 31
+
+
+def _glibc_base(seed: int) -> list:
+    """srandom_r's window s[j] = r[3 + j] (GlibcRand.seed without the discards)."""
+    word = seed & _M32
+    if word >= 0x80000000:
+        word -= 0x100000000
+    if word == 0:
+        word = 1
+    r = [word]
+    for _ in range(1, 31):
+        hi = int(word / 127773)  # C truncation
+        lo = word - hi * 127773
+        word = 16807 * lo - 2836 * hi
+        if word < 0:
+            word += 2147483647
+        r.append(word)
+    r += r[0:3]
+    return [x & _M32 for x in r[3:34]]
+
+
+def _poly_sqr(c: list) -> list:
+    p = [0] * (2 * _GDEG - 1)
+    for i in range(_GDEG):
+        ci = c[i]
+        if ci:
+            for j in range(_GDEG):
+                p[i + j] = (p[i + j] + ci * c[j]) & _M32
+    for d in range(2 * _GDEG - 2, _GDEG - 1, -1):  # x^31 = x^28 + 1
+        p[d - 3] = (p[d - 3] + p[d]) & _M32
+        p[d - _GDEG] = (p[d - _GDEG] + p[d]) & _M32
+    return p[:_GDEG]
+
+
+def _poly_mulx(c: list) -> list:
+    top = c[-1]
+    c = [top] + c[:-1]
+    c[_GDEG - 3] = (c[_GDEG - 3] + top) & _M32
+    return c
+
+
+def glibc_draws_at(seed: int, first: int, count: int) -> np.ndarray:
+    """rand() outputs first .. first+count-1 after srand(seed), by jump-ahead:
+    the window obeys s[t] = s[t-31] + s[t-3] (mod 2^32), output o is
+    s[341 + o] >> 1, and s[T] = sum c_j s[j] with x^T mod (x^31 - x^28 - 1)
+    -- the algorithm of qpb_gen.hip's ref_draws_kernel."""
+    base = _glibc_base(seed)
+    T0 = 310 + first
+    c = [1] + [0] * (_GDEG - 1)
+    for bit in range(T0.bit_length() - 1, -1, -1):
+        c = _poly_sqr(c)
+        if (T0 >> bit) & 1:
+            c = _poly_mulx(c)
+    w = []
+    for _ in range(_GDEG):
+        w.append(sum(ci * bi for ci, bi in zip(c, base)) & _M32)
+        c = _poly_mulx(c)
+    out = []
+    while len(out) < count:
+        for i in range(_GDEG):
+            w[i] = (w[i] + w[(i + _GDEG - 3) % _GDEG]) & _M32
+            if len(out) < count:
+                out.append(w[i] >> 1)
+    return np.array(out, dtype=np.float64)
+
+
+def ref_generate_at(seed: int, index: int, n: int, prange=(-1e3, 1e3), qrange=(-1e3, 1e3), xrange=(-1e3, 1e3)):
+    """QP `index` of ref_generate(seed, ...) without drawing its predecessors."""
+    D = n * n + 2 * n
+    r = glibc_draws_at(seed, index * D, D)
+
+    def rn(vals, lo, hi):
+        return lo + (vals * (hi - lo)) / RAND_MAX
+
+    B = rn(r[:n * n], *prange).reshape(n, n)
+    acc = np.zeros((n, n))
+    for k in range(n):
+        acc = acc + np.outer(B[k, :], B[k, :])
+    P = acc * (1.0 / float(prange[1] * n))
+    return P, rn(r[n * n:n * n + n], *qrange), rn(r[n * n + n:], *xrange)
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 (Salmon et al. 2011) on uint32 numpy arrays / ints."""
+    c0, c1, c2, c3 = (np.asarray(v, dtype=np.uint64) for v in (c0, c1, c2, c3))
+    k0 = np.asarray(k0, dtype=np.uint64)
+    k1 = np.asarray(k1, dtype=np.uint64)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        n0 = (p1 >> np.uint64(32)) ^ c1 ^ k0
+        n2 = (p0 >> np.uint64(32)) ^ c3 ^ k1
+        c1 = p1 & np.uint64(_M32)
+        c3 = p0 & np.uint64(_M32)
+        c0 = n0 & np.uint64(_M32)
+        c2 = n2 & np.uint64(_M32)
+        k0 = (k0 + np.uint64(0x9E3779B9)) & np.uint64(_M32)
+        k1 = (k1 + np.uint64(0xBB67AE85)) & np.uint64(_M32)
+    return c0, c1, c2, c3
+
+
+def philox_uniform(seed: int, g, purpose: int, e) -> np.ndarray:
+    """Element e of stream `purpose` of QP g in [0, 1) (qpb_gen.hip uniform())."""
+    g = np.asarray(g, dtype=np.uint64)
+    e = np.asarray(e, dtype=np.uint64)
+    g, e = np.broadcast_arrays(g, e)
+    c0, c1, c2, c3 = philox4x32_10(e >> np.uint64(1), g & np.uint64(_M32), g >> np.uint64(32),
+                                   np.full(e.shape, purpose, dtype=np.uint64), seed & _M32, (seed >> 32) & _M32)
+    odd = (e & np.uint64(1)).astype(bool)
+    hi = np.where(odd, c2, c0)
+    lo = np.where(odd, c3, c1)
+    return ((hi >> np.uint64(5)).astype(np.float64) * 67108864.0 + (lo >> np.uint64(6)).astype(np.float64)) \
+        * (1.0 / 9007199254740992.0)
+
+
+def family_generate(n: int, batch: int, seed: int, family: str = "box", m: int | None = None, first: int = 0,
+                    shift: float = 1.0, box: float = 10.0):
+    """The qpb_generate benchmark families (H by numpy matmul: equal to the
+    matrix-core product up to summation order)."""
+    m = 2 * n if m is None else m
+    g = np.arange(first, first + batch, dtype=np.uint64)[:, None]
+    B = (-1e3 + 2e3 * philox_uniform(seed, g, 0, np.arange(n * n)[None, :])).reshape(batch, n, n)
+    H = np.einsum("bki,bkj->bij", B, B) / (1e3 * n) + shift * np.eye(n)
+    f = -1e3 + 2e3 * philox_uniform(seed, g, 1, np.arange(n)[None, :])
+    if family == "box":
+        A = np.broadcast_to(np.concatenate([np.eye(n), -np.eye(n)]), (batch, 2 * n, n)).copy()
+        b = np.full((batch, 2 * n), box)
+    else:
+        e = np.arange(m * n)[None, :]
+        u1 = philox_uniform(seed, g, 2, 2 * e)
+        u2 = philox_uniform(seed, g, 2, 2 * e + 1)
+        z = (np.sqrt(-2.0 * np.log(1.0 - u1)) * np.cos(6.283185307179586 * u2)).reshape(batch, m, n)
+        A = z * (1.0 / np.sqrt((z * z).sum(axis=2, keepdims=True)))
+        b = (0.1 + 0.9 * philox_uniform(seed, g, 3, np.arange(m)[None, :])) * box
+    return H, f, A, b
