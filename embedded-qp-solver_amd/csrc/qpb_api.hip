@@ -39,6 +39,11 @@ static int fail(int code, const char *fmt, ...) {
   return code;
 }
 
+// error reporting for the host-only C parts of the library (qpb_wire.c)
+extern "C" __attribute__((visibility("hidden"))) void qpb_set_error(int code, const char *msg) {
+  fail(code, "%s", msg);
+}
+
 static int hip_fail(hipError_t e, const char *what) {
   return fail(QPB_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }

@@ -278,3 +278,42 @@ def generate(n: int, batch: int, seed: int, *, family: str = "box", m: int | Non
     _check(_lib.qpb_generate(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(A), _ptr(b), _stream_ptr(stream)),
            "qpb_generate")
     return H, f, A, b
+
+
+# ------------------------------------------------------------------ wire format
+_lib.qpb_wire_write.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64] + [_vp] * 4
+_lib.qpb_wire_write.restype = ctypes.c_int
+_lib.qpb_wire_read_header.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int32),
+                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]
+_lib.qpb_wire_read_header.restype = ctypes.c_int
+_lib.qpb_wire_read.argtypes = [ctypes.c_char_p] + [_vp] * 4
+_lib.qpb_wire_read.restype = ctypes.c_int
+
+
+def wire_write(path: str, H, f, A=None, b=None) -> None:
+    """numpy (B,n,n), (B,n)[, (B,m,n), (B,m)] -> wire file (qpb_wire_write);
+    a single unconstrained QP is written in the reference's own format."""
+    import numpy as np
+    H = np.ascontiguousarray(H, dtype=np.float64)
+    f = np.ascontiguousarray(f, dtype=np.float64)
+    B, n = f.shape
+    m = 0 if A is None else A.shape[1]
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
+    if m:
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+    _check(_lib.qpb_wire_write(os.fsencode(path), n, m, B, p(H), p(f), p(A), p(b)), "qpb_wire_write")
+
+
+def wire_read(path: str):
+    """wire file -> numpy (H, f, A, b) (A, b have m = 0 columns for an unconstrained file)."""
+    import numpy as np
+    n, m, B = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+    _check(_lib.qpb_wire_read_header(os.fsencode(path), ctypes.byref(n), ctypes.byref(m), ctypes.byref(B)),
+           "qpb_wire_read_header")
+    n, m, B = n.value, m.value, B.value
+    H, f = np.empty((B, n, n)), np.empty((B, n))
+    A, b = np.empty((B, m, n)), np.empty((B, m))
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a.size else None  # noqa: E731
+    _check(_lib.qpb_wire_read(os.fsencode(path), p(H), p(f), p(A), p(b)), "qpb_wire_read")
+    return H, f, A, b

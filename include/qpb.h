@@ -188,6 +188,19 @@ typedef struct qpb_gen_desc {
 
 int qpb_generate(const qpb_gen_desc *desc, double *H, double *f, double *A, double *b, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Wire format, host memory, native-endian fp64.
+ * The reference's single QP (test/test.c:108-126 -> test/qp_ref.py:8-30):
+ *     [n][P n*n][q n]
+ * Batched:  [n][m][B] then B records [H n*n][f n][A m*n][b m].
+ * qpb_wire_write emits the reference form when m == 0 and batch == 1; the
+ * readers accept both (told apart by the file size).                    */
+int qpb_wire_write(const char *path, int32_t n, int32_t m, int64_t batch, const double *H, const double *f,
+		   const double *A, const double *b);
+int qpb_wire_read_header(const char *path, int32_t *n, int32_t *m, int64_t *batch);
+/* H B*n*n, f B*n, A B*m*n, b B*m host buffers sized from the header */
+int qpb_wire_read(const char *path, double *H, double *f, double *A, double *b);
+
 /* housekeeping */
 int qpb_device_count(void);
 int qpb_set_device(int device);

@@ -144,6 +144,38 @@ def read_wire(path: str):
     return n, P, q
 
 
+def write_wire_batch(path: str, H: np.ndarray, f: np.ndarray, A=None, b=None) -> None:
+    """Batched wire form: fp64 [n][m][B] then B records [H][f][A][b]
+    (csrc/qpb_wire.c; the reference form when m == 0 and B == 1)."""
+    B, n = f.shape
+    m = 0 if A is None else A.shape[1]
+    if m == 0 and B == 1:
+        write_wire(path, H[0], f[0])
+        return
+    recs = [np.asarray(H, np.float64).reshape(B, -1), np.asarray(f, np.float64).reshape(B, -1)]
+    if m:
+        recs += [np.asarray(A, np.float64).reshape(B, -1), np.asarray(b, np.float64).reshape(B, -1)]
+    with open(path, "wb") as fp:
+        fp.write(np.array([n, m, B], dtype=np.float64).tobytes())
+        fp.write(np.concatenate(recs, axis=1).tobytes())
+
+
+def read_wire_batch(path: str):
+    """Either wire form -> (H (B,n,n), f (B,n), A (B,m,n), b (B,m))."""
+    vals = np.fromfile(path, dtype=np.float64)
+    n = int(vals[0])
+    if vals.size == 1 + n * n + n:
+        _, P, q = read_wire(path)
+        return P[None], q[None], np.zeros((1, 0, n)), np.zeros((1, 0))
+    m, B = int(vals[1]), int(vals[2])
+    rec = vals[3:].reshape(B, n * n + n + m * n + m)
+    H = rec[:, :n * n].reshape(B, n, n)
+    f = rec[:, n * n:n * n + n]
+    A = rec[:, n * n + n:n * n + n + m * n].reshape(B, m, n)
+    b = rec[:, n * n + n + m * n:]
+    return H.copy(), f.copy(), A.copy(), b.copy()
+
+
 def eval_qp(P, q, x):
     """qp_ref.py:5-6 (no constant term)."""
     return 0.5 * x @ P @ x + q @ x
