@@ -116,6 +116,14 @@ __device__ __forceinline__ double pack_key(double v, int idx) {
 __device__ __forceinline__ int key_index(double k) {
   return (int)(__builtin_bit_cast(unsigned long long, k) & 31ull);
 }
+// the same with a 6-bit index (one QP per 64-lane wave)
+__device__ __forceinline__ double pack_key64(double v, int idx) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  return __builtin_bit_cast(double, (b & ~63ull) | (unsigned long long)idx);
+}
+__device__ __forceinline__ int key_index64(double k) {
+  return (int)(__builtin_bit_cast(unsigned long long, k) & 63ull);
+}
 __device__ __forceinline__ double row_min(double v) {
   v = __builtin_fmin(v, ror<8>(v));
   v = __builtin_fmin(v, ror<4>(v));

@@ -1,0 +1,384 @@
+// qpb_gi_wave.hip -- active-set QP kernel for 16 < n <= 32, m <= 64 (gfx950).
+//
+// Same method as qpb_gi.hip (dual active set of Goldfarb & Idnani on
+// D = A L^{-T}, see there), mapped one QP per 64-lane wavefront: lane l owns
+// row l of D (and of H / L while factorising), every per-QP scalar is
+// wave-uniform, so control flow never diverges and no QP waits for another.
+// Broadcasts from one lane use v_readlane (SGPR results) or LDS.
+//
+// Setup, one right-looking sweep as in qpb_gi.hip, except that the pivot row
+// is gathered by symmetry: row k of the Schur complement is its column k, and
+// element k of lane j's row is a compile-time register index -- every lane
+// stores it, all lanes read the vector back (one b64 store + b128 broadcast
+// reads per step, no lane-selected writes).
+//
+// LDS per QP (one wave): L packed rows (n(n+1)/2), R column-major NP x NP with
+// zero diagonal, the pivot / exchange vector, the y / x capture.
+#include "qpb_common.h"
+#include "qpb.h"
+
+namespace qpb {
+namespace wv {
+
+constexpr int NP = 32;                              // padded n
+constexpr int L_SIZE = NP * (NP + 1) / 2;           // 528
+constexpr int OFF_L = 0;
+constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*NP + i
+constexpr int OFF_X = OFF_R + NP * NP;              // 1552: exchange row (NP) + s_p, |d|^2; pivots
+constexpr int SLOT = OFF_X + NP + 8;                // 1592 doubles = 12,736 B
+constexpr double kDepTol = 1e-24;
+
+__host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// exact min over the 64 lanes (wave-uniform result)
+__device__ __forceinline__ double wave_min(double v) {
+  v = row_min(v);
+  const double a = readlane_d(v, 0), b = readlane_d(v, 16), c = readlane_d(v, 32), d = readlane_d(v, 48);
+  return __builtin_fmin(__builtin_fmin(a, b), __builtin_fmin(c, d));
+}
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
+
+template <int N, class FX, class FY>
+__device__ __forceinline__ double dot2(FX &&x, FY &&y, double init = 0.0) {
+  double a0 = init, a1 = 0.0;
+  unroll<N>([&](auto J) {
+    constexpr int j = J;
+    if constexpr (j % 2 == 0) a0 = __builtin_fma(x(j), y(j), a0);
+    else a1 = __builtin_fma(x(j), y(j), a1);
+  });
+  return a0 + a1;
+}
+
+__device__ __forceinline__ void lds_vec(const double *src, double (&dst)[NP]) {
+#pragma unroll
+  for (int j = 0; j < NP; j += 2) {
+    const double2 v = *reinterpret_cast<const double2 *>(&src[j]);
+    dst[j] = v.x;
+    dst[j + 1] = v.y;
+  }
+}
+
+// one QP per wavefront; MR = 1 (m <= 64)
+__global__ __launch_bounds__(64, 2) void gi_wave_kernel(
+    const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
+    const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg, uint32_t *__restrict__ actg,
+    int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m, long long batch, int max_iter,
+    double feas_tol) {
+  __shared__ double lds[SLOT];
+  const int l = threadIdx.x;
+  const long long g = blockIdx.x;
+  if (g >= batch) return;
+  double *Lp = lds + OFF_L;
+  double *R = lds + OFF_R;
+  double *xch = lds + OFF_X;
+
+  const double *Hq = Hg + g * (long long)n * n;
+  const double *Aq = m > 0 ? Ag + g * (long long)m * n : Hq;
+  const double *bq = m > 0 ? bg + g * (long long)m : Hq;
+  const bool rowok = l < m;
+
+  // ------------------------------------------------------------------ load
+  // lane l reads row l of H and of A (zero padding; the sweep stops at n)
+  double Lr[NP], E[NP];
+  const double bv = bq[rowok ? l : 0];
+  const double fv = fg[g * n + (l < n ? l : 0)];
+  {
+    const int lh = l < n ? l : 0, la = rowok ? l : 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int jc = j < n ? j : 0;
+      const double h = Hq[lh * n + jc];
+      const double a = Aq[la * n + jc];
+      Lr[j] = (l < n && j < n) ? h : 0.0;
+      E[j] = (rowok && j < n) ? a : 0.0;
+    }
+  }
+
+  const double nrm2 = dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return E[j]; });
+  const double bl = rowok ? bv : 0.0;
+  const double invn = nrm2 > 0.0 ? rsq(nrm2) : 0.0;
+  double thr = (rowok && nrm2 > 0.0) ? -feas_tol * (1.0 + __builtin_fabs(bl) * invn) : -kInf;
+  const bool infeasible0 =
+      wave_any(rowok && nrm2 == 0.0 && bl < -feas_tol * (1.0 + __builtin_fabs(bl)));
+  const double fl = l < n ? fv : 0.0;
+
+  // ---- H = L L^T, D = A L^{-T}, y = L^{-1} f (right-looking, pivot row by symmetry)
+  if (l < NP) R[l] = 0.0;  // y capture (components >= n stay zero)
+  bool spd = true;
+  double ya = fl;
+  unroll<NP>([&](auto K) {
+    constexpr int k = K;
+    if (k >= n) return;  // wave-uniform: padded columns stay zero
+    __builtin_amdgcn_sched_barrier(0);
+    wave_lds_sync();
+    if (l < NP) xch[l] = Lr[k];  // column k = pivot row k (lanes >= 32 hold no H row)
+    wave_lds_sync();
+    const double akk = xch[k];
+    spd = spd && (akk > 0.0);
+    const double ik = rsq(akk);
+    const double ik2 = ik * ik;
+    const double c = Lr[k] * ik2;
+    const double e = E[k];
+    const double e2 = e * ik2;
+    Lr[k] *= ik;
+    E[k] = e * ik;
+    // the pivot row is streamed from LDS in 16-byte pairs, each pair feeding
+    // both the Schur update of row l and the substitution of D's row l
+    unroll<(NP - (k + 1) / 2 * 2) / 2>([&](auto JJ) {
+      constexpr int j = (k + 1) / 2 * 2 + 2 * JJ;
+      const double2 v = *reinterpret_cast<const double2 *>(&xch[j]);
+      if constexpr (j >= k + 1) {
+        Lr[j] = __builtin_fma(-c, v.x, Lr[j]);
+        E[j] = __builtin_fma(-e2, v.x, E[j]);
+        pin(Lr[j]);
+        pin(E[j]);
+      }
+      Lr[j + 1] = __builtin_fma(-c, v.y, Lr[j + 1]);
+      E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
+      pin(Lr[j + 1]);
+      pin(E[j + 1]);
+    });
+    const double fk = readlane_d(ya, k);
+    ya = __builtin_fma(-c, fk, ya);
+    R[k] = fk * ik;  // y_k, same-address store from every lane (R is free until the loop)
+  });
+  // L -> LDS (lane l < 32 writes row l; dead entries j > l land in later rows
+  // first and are overwritten by their owners: descending j, in-order DS;
+  // row 31's dead tail would run past L into R: clamped onto its own last entry,
+  // which its owner writes afterwards)
+  unroll<NP>([&](auto J) {
+    constexpr int j = NP - 1 - J;
+    if (l < NP) Lp[lrow(l) + j <= L_SIZE - 1 ? lrow(l) + j : L_SIZE - 1] = Lr[j];
+    wave_lds_sync();
+  });
+  // y replicated: s = b + D y, |D row|^2
+  wave_lds_sync();
+  double yv[NP];
+  lds_vec(R, yv);
+  double s = dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return yv[j]; }, bl);
+  const double dn = dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return E[j]; });
+
+  // ------------------------------------------------------ active-set loop
+  wave_lds_sync();
+  for (int j = 0; j < NP; ++j) R[j * NP + (l & (NP - 1))] = 0.0;
+  int q = 0;
+  double um = 0.0, rdg = 0.0, invRd = 0.0;
+  int iam = -1;
+  bool act = false;
+  int status = !spd ? QPB_NOT_SPD : (infeasible0 ? QPB_INFEASIBLE : QPB_MAX_ITER);
+  bool done = !spd || infeasible0;
+  bool selecting = true;
+  int p = 0;
+  double up = 0.0;
+  int it = 0;
+  wave_lds_sync();
+  while (!done && it < max_iter) {
+    ++it;
+    if (selecting) {
+      const double v = s * invn;
+      const bool viol = !act && v < thr;
+      const double key = wave_min(viol ? pack_key64(v, l) : kBig);
+      if (!(key < 0.0)) {
+        status = QPB_OK;
+        break;
+      }
+      p = __builtin_amdgcn_readfirstlane(key_index64(key));
+      up = 0.0;
+      selecting = false;
+    }
+    // row p of D, s_p, |D_p|^2 through LDS; the active columns zeroed there
+    wave_lds_sync();
+    if (l == p) {
+#pragma unroll
+      for (int j = 0; j < NP; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[j], E[j + 1]);
+      xch[NP] = s;
+      xch[NP + 1] = dn;
+    }
+    wave_lds_sync();
+    const double Dpl = xch[l & (NP - 1)];
+    const double Dpq = xch[q < NP ? q : 0];
+    const double sp = xch[NP];
+    const double dd = xch[NP + 1];
+    wave_lds_sync();
+    if (l < q) xch[l] = 0.0;
+    wave_lds_sync();
+    double d2[NP];
+    lds_vec(xch, d2);
+    const double dl = (l < NP) ? -Dpl : 0.0;
+    const double nd2 = dot2<NP>([&](int j) { return d2[j]; }, [&](int j) { return d2[j]; });
+
+    // r = R^{-1} d1 over the active positions (position j in lane j)
+    double rm = 0.0;
+    if (q > 0) {
+      double acc = (l < q) ? dl : 0.0;
+      for (int j = q - 1; j >= 0; --j) {
+        const double rj = readlane_d(acc * invRd, j);
+        acc = __builtin_fma(-R[j * NP + (l & (NP - 1))], rj, acc);
+      }
+      rm = acc * invRd;
+    }
+    double t1 = kBig;
+    int k = 0;
+    if (q > 0) {
+      const double tk = wave_min((l < q && rm > 0.0) ? pack_key64(um * rcp(rm), l) : kBig);
+      t1 = tk;
+      k = __builtin_amdgcn_readfirstlane(key_index64(tk));
+    }
+    const double t2 = (nd2 > kDepTol * dd) ? -sp * rcp(nd2) : kBig;
+    const double t = t1 < t2 ? t1 : t2;
+    if (!(t < kBig)) {
+      status = QPB_INFEASIBLE;
+      break;
+    }
+    if (t2 < kBig) s = __builtin_fma(t, dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return d2[j]; }), s);
+    pin(s);
+    um = __builtin_fma(-t, rm, um);
+    up += t;
+
+    if (t2 <= t1) {
+      // ADD p (Householder on columns q.., v = d2 + alpha e_q as in qpb_gi.hip)
+      const double nrm = nd2 * rsq(nd2);
+      const double alpha = Dpq <= 0.0 ? -nrm : nrm;
+      const double beta = rcp(__builtin_fma(alpha, Dpq, nd2));
+      wave_lds_sync();
+      if (l == q) xch[q] = Dpq + alpha;
+      wave_lds_sync();
+      double v[NP];
+      lds_vec(xch, v);
+      const double w = beta * dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return v[j]; });
+#pragma unroll
+      for (int j = 0; j < NP; ++j) E[j] = __builtin_fma(-w, v[j], E[j]);
+      if (l < NP) R[q * NP + l] = (l < q) ? dl : 0.0;
+      if (l == q) {
+        rdg = alpha;
+        invRd = rcp(alpha);
+        iam = p;
+        um = up;
+      }
+      if (l == p) act = true;
+      ++q;
+      selecting = true;
+    } else {
+      // DROP active position k
+      const int c = __builtin_amdgcn_readlane(iam, k);
+      if (l == c) act = false;
+      const double un = __shfl(um, (l + 1) & 63);
+      const int in = __shfl(iam, (l + 1) & 63);
+      if (l >= k && l < q - 1) {
+        um = un;
+        iam = in;
+      } else if (l == q - 1) {
+        um = 0.0;
+        iam = -1;
+      }
+      const int lc = l & (NP - 1);
+      wave_lds_sync();
+      if (l < q) R[l * NP + l] = rdg;
+      const bool shift = l >= k && l < q - 1;
+      for (int i = 0; i < q; ++i) {
+        wave_lds_sync();
+        const double nxt = R[((lc + 1) & (NP - 1)) * NP + i];
+        wave_lds_sync();
+        if (shift) R[l * NP + i] = nxt;
+        else if (l == q - 1) R[l * NP + i] = 0.0;
+      }
+      for (int j = k; j < q - 1; ++j) {
+        wave_lds_sync();
+        const double a = R[j * NP + j], bb = R[j * NP + j + 1];
+        const double ir = rsq(__builtin_fma(a, a, bb * bb));
+        const double cj = a * ir, sj = bb * ir;
+        const double rj = R[lc * NP + j], rj1 = R[lc * NP + j + 1];
+        wave_lds_sync();
+        if (l >= j && l < q - 1) {
+          R[l * NP + j] = __builtin_fma(cj, rj, sj * rj1);
+          R[l * NP + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
+        }
+        // the same rotation on columns j, j+1 of D (j wave-uniform)
+        unroll<NP - 1>([&](auto JJ) {
+          constexpr int jj = JJ;
+          if (jj == j) {
+            const double e0 = E[jj], e1 = E[jj + 1];
+            E[jj] = __builtin_fma(cj, e0, sj * e1);
+            E[jj + 1] = __builtin_fma(-sj, e0, cj * e1);
+          }
+        });
+      }
+      wave_lds_sync();
+      if (l < NP) R[l * NP + q - 1] = 0.0;
+      --q;
+      wave_lds_sync();
+      const double dg = (l < q) ? R[l * NP + l] : 0.0;
+      wave_lds_sync();
+      if (l < q) R[l * NP + l] = 0.0;
+      rdg = dg;
+      invRd = (l < q) ? rcp(dg) : 0.0;
+    }
+  }
+
+  // ------------------------------------------------------------- outputs
+  // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iact_k}, then L y = g,
+  // L^T x = -y lane-parallel (L read from LDS, broadcasts by v_readlane)
+  double gl = fl;
+  for (int kk = 0; kk < q; ++kk) {
+    const int row = __builtin_amdgcn_readlane(iam, kk);
+    const double u = readlane_d(um, kk);
+    gl = __builtin_fma(u, (l < n) ? Aq[row * n + (l < n ? l : 0)] : 0.0, gl);
+  }
+  const int ll = l & (NP - 1);
+  wave_lds_sync();
+  const double invd = ll < n ? rcp(Lp[lrow(ll) + ll]) : 0.0;
+  double acc = gl;
+  double yl = 0.0;
+  for (int kk = 0; kk < n; ++kk) {
+    const double yk = readlane_d(acc * invd, kk);
+    if (l == kk) yl = yk;
+    acc = __builtin_fma(-((ll > kk) ? Lp[lrow(ll) + kk] : 0.0), yk, acc);
+  }
+  acc = yl;
+  double xl = 0.0;
+  for (int kk = n - 1; kk >= 0; --kk) {
+    const double xk = readlane_d(acc * invd, kk);
+    if (l == kk) xl = xk;
+    acc = __builtin_fma(-((ll < kk) ? Lp[lrow(kk) + ll] : 0.0), xk, acc);
+  }
+  xl = -xl;
+  if (status == QPB_OK && wave_any(l < n && !(__builtin_fabs(xl) < kInf))) status = QPB_NUMERICAL;
+  // lambda scatter through LDS (64 entries over xch + the start of R)
+  wave_lds_sync();
+  double *lamb = R;
+  lamb[l] = 0.0;
+  wave_lds_sync();
+  if (l < q && iam >= 0) lamb[iam] = um;
+  wave_lds_sync();
+  if (rowok) lamg[g * m + l] = lamb[l];
+  if (l < n) xg[g * n + l] = xl;
+  const unsigned long long bal = __ballot(act);
+  if (l == 0) {
+    if (m > 0) {
+      const int words = (m + 31) / 32;
+      actg[g * words] = (uint32_t)bal;
+      if (words > 1) actg[g * words + 1] = (uint32_t)(bal >> 32);
+    }
+    statg[g] = status;
+    if (itg) itg[g] = it;
+  }
+}
+
+}  // namespace wv
+}  // namespace qpb
+
+extern "C" hipError_t qpb_launch_gi_wave(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                         const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
+                                         int32_t *iters, hipStream_t stream) {
+  const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
+  const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
+  hipLaunchKernelGGL(qpb::wv::gi_wave_kernel, dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b, x, lam,
+                     active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol);
+  return hipGetLastError();
+}

@@ -55,9 +55,11 @@ extern "C" {
 #define QPB_VERSION_MAJOR 0
 #define QPB_VERSION_MINOR 2
 
-/* limits of this build's kernels (n <= 16: one QP per 16-lane DPP row) */
-#define QPB_MAX_N 16
-#define QPB_MAX_M 32
+/* limits of this build's kernels: n <= 16, m <= 32 one QP per 16-lane DPP
+ * row (qpb_gi.hip); otherwise n <= 32, m <= 64 one QP per wavefront
+ * (qpb_gi_wave.hip) */
+#define QPB_MAX_N 32
+#define QPB_MAX_M 64
 
 typedef enum qpb_status {
 	QPB_OK = 0,         /* KKT point found (within feas_tol) */
