@@ -31,6 +31,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
 
+BASELINE_METRIC = "QPs/sec (whole node) at n=16,m=32 batch=1M; % HBM roofline at 1/2/4/8 GPUs"  # BASELINE.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 
 
@@ -46,6 +47,17 @@ def make_batch(torch, B: int, n: int, family: str, seed: int, device, first: int
     the matching slice of one big batch)."""
     import qpb
     return qpb.generate(n, B, seed, family=family, first=first, shift=1.0, box=box, device=device)
+
+
+def baseline_config(n: int, total: int, world: int) -> str:
+    """Which BASELINE.json config a run measures (configs[1] is the headline)."""
+    if n == 16 and total == 65536 and world == 1:
+        return "BASELINE configs[1]"
+    if n == 16 and total == 1048576:
+        return "BASELINE configs[2]"
+    if n == 32 and total == 262144:
+        return "BASELINE configs[4] shape, fp64 throughout"
+    return "not a BASELINE config"
 
 
 def pmc_traffic(n: int, m: int, B: int, family: str, library: str):
@@ -221,7 +233,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "QPs/sec (whole node) at n=16,m=32; % HBM roofline",
+            "metric": (BASELINE_METRIC if (n, m) == (16, 32) else f"QPs/sec (whole node) at n={n},m={m}; % HBM roofline"),
             "value": value,
             "unit": "QPs/s",
             "n_gpus": world,
@@ -236,14 +248,15 @@ def main():
                     f"conditioned {args.family} family of SURVEY.md §8d",
             "config": {"workload": f"batched active-set QP solve, n={n}, m={m} "
                                    f"({'box as dense A=[I;-I]' if args.family == 'box' else 'dense random A'}), "
-                                   f"{B} QPs per GPU (BASELINE configs[1])",
+                                   f"{B} QPs per GPU ({baseline_config(n, total_B, world)})",
                        "n": n, "m": m, "batch_per_gpu": B, "global_batch": total_B,
                        "family": args.family, "parallelism": f"qp-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": "qpb::gi_dense_kernel<2, true, true, false, 3>", "bytes_per_qp": bpq,
+                         "kernel": ("qpb::gi_dense_kernel<2, true, true, false, 3>" if n <= 16 and m <= 32
+                                    else "qpb::wv::gi_wave_kernel"), "bytes_per_qp": bpq,
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
