@@ -20,6 +20,9 @@ extern "C" hipError_t qpb_launch_gi_sections(const qpb_desc *d, const double *H,
 extern "C" hipError_t qpb_launch_gi_wave(const qpb_desc *d, const double *H, const double *f, const double *A,
                                          const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
                                          int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_block(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                          const double *b, double *x, double *lam, uint32_t *active,
+                                          int32_t *status, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q,
                                      const double *x0, double *x, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
@@ -80,10 +83,15 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
     return fail(QPB_ERR_INVALID_ARG, "A, b, lam and active are required when m > 0");
   rc = check_device();
   if (rc) return rc;
-  // n <= 16, m <= 32: four QPs per wavefront; larger: one QP per wavefront
-  hipError_t e = (d->n <= 16 && d->m <= 32)
-                     ? qpb_launch_gi(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream)
-                     : qpb_launch_gi_wave(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
+  // n <= 16, m <= 32: four QPs per wavefront; n <= 32, m <= 64: one QP per
+  // wavefront; larger: one QP per workgroup
+  hipError_t e;
+  if (d->n <= 16 && d->m <= 32)
+    e = qpb_launch_gi(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
+  else if (d->n <= 32 && d->m <= 64)
+    e = qpb_launch_gi_wave(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
+  else
+    e = qpb_launch_gi_block(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
   return 0;
 }

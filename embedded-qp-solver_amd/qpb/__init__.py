@@ -39,7 +39,7 @@ STATUS_NAMES = {OK: "OK", MAX_ITER: "MAX_ITER", NOT_SPD: "NOT_SPD", INFEASIBLE: 
 ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_DEVICE = -1, -2, -3, -4
 # reference modes (qpb_ref_mode)
 REF_NEWTON, REF_ADMM, REF_GD = 1, 2, 3
-MAX_N, MAX_M = 32, 64
+MAX_N, MAX_M = 128, 256
 
 
 class Desc(ctypes.Structure):

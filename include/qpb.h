@@ -56,10 +56,10 @@ extern "C" {
 #define QPB_VERSION_MINOR 2
 
 /* limits of this build's kernels: n <= 16, m <= 32 one QP per 16-lane DPP
- * row (qpb_gi.hip); otherwise n <= 32, m <= 64 one QP per wavefront
- * (qpb_gi_wave.hip) */
-#define QPB_MAX_N 32
-#define QPB_MAX_M 64
+ * row (qpb_gi.hip); n <= 32, m <= 64 one QP per wavefront (qpb_gi_wave.hip);
+ * n <= 128, m <= 256 one QP per 1024-thread workgroup (qpb_gi_block.hip) */
+#define QPB_MAX_N 128
+#define QPB_MAX_M 256
 
 typedef enum qpb_status {
 	QPB_OK = 0,         /* KKT point found (within feas_tol) */

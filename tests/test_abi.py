@@ -66,7 +66,7 @@ def test_argument_errors_without_gpu():
     vp = ctypes.c_void_p
     lib.qpb_solve.argtypes = [ctypes.POINTER(Desc)] + [vp] * 10
     # invalid sizes are rejected before any device work
-    d = Desc(33, 32, 10, 0, 0, 0.0)
+    d = Desc(129, 32, 10, 0, 0, 0.0)
     assert lib.qpb_solve(ctypes.byref(d), *([None] * 10)) == -2  # QPB_ERR_UNSUPPORTED
     d = Desc(0, 0, 10, 0, 0, 0.0)
     assert lib.qpb_solve(ctypes.byref(d), *([None] * 10)) == -1  # QPB_ERR_INVALID_ARG
