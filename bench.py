@@ -57,6 +57,8 @@ def baseline_config(n: int, total: int, world: int) -> str:
         return "BASELINE configs[2]"
     if n == 32 and total == 262144:
         return "BASELINE configs[4] shape, fp64 throughout"
+    if n == 128 and total == 16384:
+        return "BASELINE configs[3]"
     return "not a BASELINE config"
 
 
@@ -256,7 +258,8 @@ def main():
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel": ("qpb::gi_dense_kernel<2, true, true, false, 3>" if n <= 16 and m <= 32
-                                    else "qpb::wv::gi_wave_kernel"), "bytes_per_qp": bpq,
+                                    else "qpb::wv::gi_wave_kernel" if n <= 32 and m <= 64
+                                    else "qpb::blk::gi_block_kernel"), "bytes_per_qp": bpq,
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},

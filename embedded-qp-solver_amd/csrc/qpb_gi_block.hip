@@ -96,11 +96,15 @@ __device__ bool chol_lds(double *M, double *X, int n, int tid) {
     __syncthreads();
     if (tid == 0) M[k * NB + k] = akk * ik;
     for (int i = k + 1 + tid; i < n; i += NT) M[i * NB + k] = X[i];
-    // trailing lower triangle: (i, j), k < j <= i < n
-    const int w = n - k - 1;
-    for (int e = tid; e < w * w; e += NT) {
-      const int i = k + 1 + e / w, j = k + 1 + e % w;
-      if (j <= i) M[i * NB + j] = __builtin_fma(-X[i], X[j], M[i * NB + j]);
+    // trailing lower triangle (i, j), k < j <= i < n: thread t takes column
+    // k + 1 + (t mod 128) and every 8th row from k + 1 + t / 128
+    {
+      const int j = k + 1 + (tid & (NB - 1));
+      if (j < n) {
+        const double xj = X[j];
+        for (int i = k + 1 + (tid >> 7); i < n; i += NT / NB)
+          if (j <= i) M[i * NB + j] = __builtin_fma(-X[i], xj, M[i * NB + j]);
+      }
     }
     __syncthreads();
   }

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Kernel times of the BASELINE configs beyond the headline one (HIP events,
+median of R launches) with the max_iter ablation (setup + one iteration vs
+the full solve): configs[3] n=128 m=256 B=16,384, configs[4] shape n=32
+m=64 B=262,144 (fp64), and the headline n=16 m=32 B=65,536 for reference."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import qpb  # noqa: E402
+
+
+def t_kernel(fn, reps=5):
+    s = torch.cuda.current_stream()
+    fn()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    out = {}
+    for name, n, B, fam, reps in (("c1_n16_m32", 16, 65536, "box", 9), ("c4_n32_m64", 32, 262144, "dense", 5),
+                                  ("c3_n128_m256", 128, 16384, "box", 3)):
+        H, f, A, b = qpb.generate(n, B, 20261015, family=fam)
+        sol = qpb.solve(H, f, A, b)
+        torch.cuda.synchronize()
+        it = sol.iters.double()
+        ms = t_kernel(lambda: qpb.solve(H, f, A, b, out=sol), reps)
+        ms1 = t_kernel(lambda: qpb.solve(H, f, A, b, max_iter=1, out=sol), reps)
+        bpq = bench.bytes_per_qp(n, 2 * n)
+        out[name] = {"n": n, "m": 2 * n, "batch": B, "family": fam, "kernel_ms": ms, "maxit1_ms": ms1,
+                     "qps_per_s": B / (ms * 1e-3), "achieved_GBs": B * bpq / (ms * 1e-3) / 1e9,
+                     "frac_of_8TBs": B * bpq / (ms * 1e-3) / 8e12, "iters_mean": float(it.mean()),
+                     "iters_max": int(it.max())}
+        print(name, json.dumps(out[name]), file=sys.stderr, flush=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
