@@ -180,7 +180,7 @@ __device__ __forceinline__ void gi_group(
   const double *bq = m > 0 ? bg + gi * (long long)m : Hq;
   double Lr[NL];  // row l of H, becomes row l of L
   double E[MR][NL];
-  double s[MR], invn[MR], bl[MR], dn[MR], thr[MR];
+  double s[MR], invn[MR], bl[MR], thr[MR];
   bool act[MR];
   bool infeasible_row = false;
   // b and f with the matrices (same round trip)
@@ -324,7 +324,6 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
     for (int r = 0; r < MR; ++r) {
       s[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return yv[j]; }, bl[r]);
-      dn[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
     }
   }
   clk.tick(1);
@@ -405,14 +404,13 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
           for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[r][j], E[r][j + 1]);
           xch[NL] = s[r];
-          xch[NL + 1] = dn[r];
         }
     }
     wave_lds_sync();
     const double Dpl = xch[l];
     const double Dpq = xch[q];  // q == 16 reads s_p: only used by an ADD, impossible then
     const double sp = xch[NL];
-    const double dd = xch[NL + 1];  // |D[p,:]|^2 (invariant under the column rotations)
+
     wave_lds_sync();
     if (l < q) xch[l] = 0.0;
     wave_lds_sync();
@@ -420,6 +418,7 @@ __device__ __forceinline__ void gi_group(
     lds_row16(xch, d2);
     const double dl = -Dpl;  // d1 component of active position l
     const double nd2 = row_sum(l >= q ? Dpl * Dpl : 0.0);  // |d2|^2
+    const double dd = row_sum(Dpl * Dpl);                   // |D[p,:]|^2
     clk.tick(5);
 
     // ---- r = R^{-1} d1: lane-parallel back substitution over the active positions
@@ -442,7 +441,8 @@ __device__ __forceinline__ void gi_group(
       t1 = tk;
       k = key_index(tk);
     }
-    const double t2 = (nd2 > kDepTol * dd) ? -sp * rcp(nd2) : kBig;
+    const double ir = rsq(nd2);  // 1/|d2| (only used when nd2 > 0)
+    const double t2 = (nd2 > kDepTol * dd) ? -sp * (ir * ir) : kBig;
     const double t = t1 < t2 ? t1 : t2;
     if (!(t < kBig)) {
       status = QPB_INFEASIBLE;
@@ -464,9 +464,10 @@ __device__ __forceinline__ void gi_group(
       // ---------------- ADD p: Householder on columns q.. of D.  With
       // dq = -D[p,q]: alpha = -sign(dq) |d2|, v = d2 + alpha e_q (the negated
       // G-I vector: same reflection), beta = 1 / (|d2|^2 + alpha D[p,q]).
-      const double nrm = nd2 * rsq(nd2);  // nd2 > 0 here
+      // nd2 + alpha D[p,q] = |d2| (|d2| + |D[p,q]|): one reciprocal
+      const double nrm = nd2 * ir;
       const double alpha = Dpq <= 0.0 ? -nrm : nrm;
-      const double beta = rcp(__builtin_fma(alpha, Dpq, nd2));
+      const double beta = ir * rcp(nrm + __builtin_fabs(Dpq));
       if (l == q) xch[q] = Dpq + alpha;
       wave_lds_sync();
       double v[NL];
@@ -481,7 +482,7 @@ __device__ __forceinline__ void gi_group(
       R[q * NL + l] = (l < q) ? dl : 0.0;
       if (l == q) {
         rdg = alpha;
-        invRd = rcp(alpha);
+        invRd = Dpq <= 0.0 ? -ir : ir;  // 1 / alpha
         iam = p;
         um = up;
       }
