@@ -171,10 +171,18 @@ def main():
         Hc, fc, _, _ = oracle.family_generate(args.n, args.cpu_sample, args.seed, "box")
         cpu = cpu_baseline(Hc, fc, args.cpu_seconds, procs)
         del Hc, fc
+    # one GPU per rank; QPB_DIST_BACKEND=gloo (with ranks sharing a card) rehearses
+    # the N>1 path on a one-GPU box -- the driver's runs use RCCL ("nccl")
+    backend = os.environ.get("QPB_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     import qpb
