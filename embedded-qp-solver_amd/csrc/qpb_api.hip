@@ -17,6 +17,10 @@ extern "C" hipError_t qpb_launch_gi_sections(const qpb_desc *d, const double *H,
                                              const double *b, double *x, double *lam, uint32_t *active,
                                              int32_t *status, int32_t *iters, unsigned long long *sections,
                                              hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_wave_sections(const qpb_desc *d, const double *H, const double *f,
+                                                  const double *A, const double *b, double *x, double *lam,
+                                                  uint32_t *active, int32_t *status, int32_t *iters,
+                                                  unsigned long long *sections, hipStream_t stream);
 extern "C" hipError_t qpb_launch_gi_wave(const qpb_desc *d, const double *H, const double *f, const double *A,
                                          const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
                                          int32_t *iters, hipStream_t stream);
@@ -102,10 +106,15 @@ extern "C" int qpb_solve_sections(const qpb_desc *d, const double *H, const doub
   int rc = check_desc(d);
   if (rc) return rc;
   if (d->batch == 0) return 0;
-  if (d->n != 16 || d->m <= 16 || !sections) return fail(QPB_ERR_UNSUPPORTED, "sections: n=16, 16<m<=32 only");
+  const bool n16 = d->n == 16 && d->m > 16 && d->m <= 32, wave = d->n > 16 && d->n <= 32 && d->m <= 64;
+  if (!(n16 || wave) || !sections)
+    return fail(QPB_ERR_UNSUPPORTED, "sections: n=16 with 16<m<=32, or 16<n<=32 with m<=64");
   rc = check_device();
   if (rc) return rc;
-  hipError_t e = qpb_launch_gi_sections(d, H, f, A, b, x, lam, active, status, iters, sections, (hipStream_t)stream);
+  hipError_t e = n16 ? qpb_launch_gi_sections(d, H, f, A, b, x, lam, active, status, iters, sections,
+                                              (hipStream_t)stream)
+                     : qpb_launch_gi_wave_sections(d, H, f, A, b, x, lam, active, status, iters, sections,
+                                                   (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "qpb_solve_sections launch");
   return 0;
 }

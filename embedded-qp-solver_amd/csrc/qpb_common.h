@@ -157,4 +157,37 @@ __device__ __forceinline__ int wave_max4(int v) {
   return ab > cd ? ab : cd;
 }
 
+// Diagnostic builds only (STAMP = true, qpb_solve_sections): s_memrealtime stamps
+// (100 MHz) accumulate each wave's ticks per kernel section; the real kernels have none.
+constexpr int kSections = 12;
+template <bool ON>
+struct SectionClock {
+  __device__ __forceinline__ void tick(int) {}
+  __device__ __forceinline__ void flush(unsigned long long *) {}
+};
+template <>
+struct SectionClock<true> {
+  unsigned long long last, acc[kSections];
+  __device__ __forceinline__ unsigned long long now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  }
+  __device__ __forceinline__ SectionClock() {
+    for (int i = 0; i < kSections; ++i) acc[i] = 0;
+    last = now();
+  }
+  __device__ __forceinline__ void tick(int i) {
+    const unsigned long long t = now();
+    acc[i] += t - last;
+    last = t;
+  }
+  __device__ __forceinline__ void flush(unsigned long long *dbg) {
+    if ((threadIdx.x & 63) == 0)
+      for (int i = 0; i < kSections; ++i) atomicAdd(&dbg[i], acc[i]);
+  }
+};
+
 }  // namespace qpb

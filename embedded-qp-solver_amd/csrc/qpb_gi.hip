@@ -70,39 +70,6 @@ constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
 static_assert(SLOT % 2 == 0 && OFF_R % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
 static_assert(NL * RS <= SLOT - OFF_R, "input transposes are staged in R + xch");
 
-// Diagnostic build only (STAMP = true, qpb_solve_sections): s_memrealtime stamps (100 MHz)
-// accumulate each wave's ticks per kernel section; the real kernel has none.
-constexpr int kSections = 12;
-template <bool ON>
-struct SectionClock {
-  __device__ __forceinline__ void tick(int) {}
-  __device__ __forceinline__ void flush(unsigned long long *) {}
-};
-template <>
-struct SectionClock<true> {
-  unsigned long long last, acc[kSections];
-  __device__ __forceinline__ unsigned long long now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-  }
-  __device__ __forceinline__ SectionClock() {
-    for (int i = 0; i < kSections; ++i) acc[i] = 0;
-    last = now();
-  }
-  __device__ __forceinline__ void tick(int i) {
-    const unsigned long long t = now();
-    acc[i] += t - last;
-    last = t;
-  }
-  __device__ __forceinline__ void flush(unsigned long long *dbg) {
-    if ((threadIdx.x & 63) == 0)
-      for (int i = 0; i < kSections; ++i) atomicAdd(&dbg[i], acc[i]);
-  }
-};
-
 // sum_{j<N} x(j) y(j) with 2 independent accumulators
 template <int N, class FX, class FY>
 __device__ __forceinline__ double dot2(FX &&x, FY &&y, double init = 0.0) {

@@ -14,6 +14,8 @@
 //
 // LDS per QP (one wave): L packed rows (n(n+1)/2), R column-major NP x NP with
 // zero diagonal, the pivot / exchange vector, the y / x capture.
+#include <type_traits>
+
 #include "qpb_common.h"
 #include "qpb.h"
 
@@ -64,13 +66,32 @@ __device__ __forceinline__ void lds_vec(const double *src, double (&dst)[NP]) {
   }
 }
 
-// one QP per wavefront; MR = 1 (m <= 64)
-__global__ __launch_bounds__(64, 2) void gi_wave_kernel(
+// sum over lanes 0-31 (wave-uniform)
+__device__ __forceinline__ double half_sum(double v) {
+  v = row_sum(v);
+  return readlane_d(v, 0) + readlane_d(v, 16);
+}
+// E . (vector in LDS), two accumulators
+__device__ __forceinline__ double dot_xch(const double (&E)[NP], const double *x) {
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NP; j += 2) {
+    const double2 v = *reinterpret_cast<const double2 *>(&x[j]);
+    a0 = __builtin_fma(E[j], v.x, a0);
+    a1 = __builtin_fma(E[j + 1], v.y, a1);
+  }
+  return a0 + a1;
+}
+
+// one QP per wavefront; MR = 1 (m <= 64); OCC waves per SIMD
+template <int OCC, bool STAMP = false>
+__global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg, uint32_t *__restrict__ actg,
     int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m, long long batch, int max_iter,
-    double feas_tol) {
+    double feas_tol, unsigned long long *__restrict__ dbg = nullptr) {
   __shared__ double lds[SLOT];
+  SectionClock<STAMP> clk;
   const int l = threadIdx.x;
   const long long g = blockIdx.x;
   if (g >= batch) return;
@@ -84,22 +105,82 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
   const bool rowok = l < m;
 
   // ------------------------------------------------------------------ load
-  // lane l reads row l of H and of A (zero padding; the sweep stops at n)
+  // H and A are read flat and coalesced (lane l takes element i*64 + l: a
+  // row-per-lane read would touch 64 cache lines per instruction and, with
+  // eight QPs in flight per CU, thrash the vector L1), staged in LDS as rows
+  // of stride NP + 2 doubles (16-byte aligned rows, conflict-free b128 row
+  // reads) and read back one row per lane: A rows 0-31, A rows 32-63, then H
+  // (each part at most 32 rows = 16 loads of 64 lanes).
   double Lr[NP], E[NP];
   const double bv = bq[rowok ? l : 0];
   const double fv = fg[g * n + (l < n ? l : 0)];
   {
-    const int lh = l < n ? l : 0, la = rowok ? l : 0;
+    constexpr int RST = NP + 2;  // staged row stride
+    const int nn = n * n, h0 = (m < NP ? m : NP) * n, h1 = m * n - h0;  // A rows 0-31 | 32-63
+    double hv[16], av[2][16];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int jc = j < n ? j : 0;
-      const double h = Hq[lh * n + jc];
-      const double a = Aq[la * n + jc];
-      Lr[j] = (l < n && j < n) ? h : 0.0;
-      E[j] = (rowok && j < n) ? a : 0.0;
+    for (int i = 0; i < 16; ++i) {
+      const int e = i * 64 + l;
+      // clamped, not masked: lane-vs-runtime compares would be hoisted into
+      // SGPR masks; elements past the end land in rows nobody reads
+      hv[i] = Hq[min(e, nn - 1)];
+      av[0][i] = Aq[max(min(e, h0 - 1), 0)];
+      av[1][i] = Aq[max(h0 + min(e, h1 - 1), 0)];
     }
+    // flat element e = i*64 + l -> (row, col) of an n-column matrix, stepped
+    // per i by 64 = q0*n + r0 (n > 16, so one wrap per step at most)
+    const int q0 = 64 / n, r0 = 64 - q0 * n;
+    const int rl = l / n, cl = l - rl * n;
+    auto stage = [&](const double (&v)[16]) {
+      int r = rl, c = cl;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        lds[min(r, NP) * RST + c] = v[i];  // rows >= the part's own: unread
+        c += r0;
+        r += q0;
+        if (c >= n) {
+          c -= n;
+          ++r;
+        }
+      }
+    };
+    auto fetch_row = [&](double (&dst)[NP], int row, bool keep) {
+      if (keep) {
+#pragma unroll
+        for (int j = 0; j < NP; j += 2) {
+          const double2 v = *reinterpret_cast<const double2 *>(&lds[row * RST + j]);
+          dst[j] = v.x;
+          dst[j + 1] = v.y;
+        }
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < NP; ++j) Lr[j] = E[j] = 0.0;
+    // columns >= n of the staging rows stay zero for all three parts
+#pragma unroll
+    for (int i = 0; i < (NP * RST + 127) / 128; ++i)
+      if (i * 128 + 2 * l < (NP + 1) * RST)
+        *reinterpret_cast<double2 *>(&lds[i * 128 + 2 * l]) = make_double2(0.0, 0.0);
+    wave_lds_sync();
+    // A first: the 64 loaded registers of A are released before L's 64 are
+    // filled (peak E + L + H's 32 staged values, not E + L + A)
+    stage(av[0]);
+    wave_lds_sync();
+    fetch_row(E, l & (NP - 1), l < NP && rowok);
+    wave_lds_sync();
+    if (m > NP) {
+      stage(av[1]);
+      wave_lds_sync();
+      fetch_row(E, l & (NP - 1), l >= NP && rowok);
+      wave_lds_sync();
+    }
+    stage(hv);
+    wave_lds_sync();
+    fetch_row(Lr, l & (NP - 1), l < n);
+    wave_lds_sync();
   }
 
+  clk.tick(0);  // load
   const double nrm2 = dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return E[j]; });
   const double bl = rowok ? bv : 0.0;
   const double invn = nrm2 > 0.0 ? rsq(nrm2) : 0.0;
@@ -129,25 +210,56 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
     Lr[k] *= ik;
     E[k] = e * ik;
     // the pivot row is streamed from LDS in 16-byte pairs, each pair feeding
-    // both the Schur update of row l and the substitution of D's row l
-    unroll<(NP - (k + 1) / 2 * 2) / 2>([&](auto JJ) {
-      constexpr int j = (k + 1) / 2 * 2 + 2 * JJ;
-      const double2 v = *reinterpret_cast<const double2 *>(&xch[j]);
-      if constexpr (j >= k + 1) {
-        Lr[j] = __builtin_fma(-c, v.x, Lr[j]);
-        E[j] = __builtin_fma(-e2, v.x, E[j]);
-        pin(Lr[j]);
-        pin(E[j]);
-      }
-      Lr[j + 1] = __builtin_fma(-c, v.y, Lr[j + 1]);
-      E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
-      pin(Lr[j + 1]);
-      pin(E[j + 1]);
-    });
+    // both the Schur update of row l and the substitution of D's row l.
+    // pin() is a scheduling barrier, so the reads go in groups of GP pairs,
+    // double-buffered: group g+1 is in flight while group g is applied (one
+    // exposed LDS latency per step instead of one per pair)
+    constexpr int j0 = (k + 1) / 2 * 2, NPAIR = (NP - j0) / 2, GP = 4, NG = (NPAIR + GP - 1) / GP;
+    if constexpr (NPAIR > 0) {
+      double2 buf[2][GP];
+      auto fetch = [&](auto G) {
+        constexpr int g = G;
+        unroll<GP>([&](auto I) {
+          constexpr int pr = g * GP + I;
+          if constexpr (pr < NPAIR) buf[g & 1][I] = *reinterpret_cast<const double2 *>(&xch[j0 + 2 * pr]);
+        });
+      };
+      fetch(std::integral_constant<int, 0>{});
+      unroll<NG>([&](auto G) {
+        constexpr int g = G;
+        if constexpr (g + 1 < NG) fetch(std::integral_constant<int, g + 1>{});
+        unroll<GP>([&](auto I) {
+          constexpr int pr = g * GP + I;
+          if constexpr (pr < NPAIR) {
+            constexpr int j = j0 + 2 * pr;
+            const double2 v = buf[g & 1][I];
+            if constexpr (j >= k + 1) {
+              Lr[j] = __builtin_fma(-c, v.x, Lr[j]);
+              E[j] = __builtin_fma(-e2, v.x, E[j]);
+            }
+            Lr[j + 1] = __builtin_fma(-c, v.y, Lr[j + 1]);
+            E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
+          }
+        });
+        unroll<GP>([&](auto I) {
+          constexpr int pr = g * GP + I;
+          if constexpr (pr < NPAIR) {
+            constexpr int j = j0 + 2 * pr;
+            if constexpr (j >= k + 1) {
+              pin(Lr[j]);
+              pin(E[j]);
+            }
+            pin(Lr[j + 1]);
+            pin(E[j + 1]);
+          }
+        });
+      });
+    }
     const double fk = readlane_d(ya, k);
     ya = __builtin_fma(-c, fk, ya);
     R[k] = fk * ik;  // y_k, same-address store from every lane (R is free until the loop)
   });
+  clk.tick(1);  // sweep
   // L -> LDS (lane l < 32 writes row l; dead entries j > l land in later rows
   // first and are overwritten by their owners: descending j, in-order DS;
   // row 31's dead tail would run past L into R: clamped onto its own last entry,
@@ -178,6 +290,7 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
   double up = 0.0;
   int it = 0;
   wave_lds_sync();
+  clk.tick(2);  // L store, s, |D row|^2
   while (!done && it < max_iter) {
     ++it;
     if (selecting) {
@@ -192,6 +305,7 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
       up = 0.0;
       selecting = false;
     }
+    clk.tick(3);  // select
     // row p of D, s_p, |D_p|^2 through LDS; the active columns zeroed there
     wave_lds_sync();
     if (l == p) {
@@ -207,12 +321,12 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
     const double dd = xch[NP + 1];
     wave_lds_sync();
     if (l < q) xch[l] = 0.0;
-    wave_lds_sync();
-    double d2[NP];
-    lds_vec(xch, d2);
+    // |d2|^2 from the lanes' own entries (lanes 0-31; rows 2, 3 repeat them)
+    const double nd2 = half_sum((l & (NP - 1)) >= q ? Dpl * Dpl : 0.0);
     const double dl = (l < NP) ? -Dpl : 0.0;
-    const double nd2 = dot2<NP>([&](int j) { return d2[j]; }, [&](int j) { return d2[j]; });
+    wave_lds_sync();
 
+    clk.tick(4);  // exchange
     // r = R^{-1} d1 over the active positions (position j in lane j)
     double rm = 0.0;
     if (q > 0) {
@@ -223,6 +337,7 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
       }
       rm = acc * invRd;
     }
+    clk.tick(5);  // back solve
     double t1 = kBig;
     int k = 0;
     if (q > 0) {
@@ -236,11 +351,13 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
       status = QPB_INFEASIBLE;
       break;
     }
-    if (t2 < kBig) s = __builtin_fma(t, dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return d2[j]; }), s);
+    // d2 is streamed from the exchange row (broadcast reads), not held
+    if (t2 < kBig) s = __builtin_fma(t, dot_xch(E, xch), s);
     pin(s);
     um = __builtin_fma(-t, rm, um);
     up += t;
 
+    clk.tick(6);  // step
     if (t2 <= t1) {
       // ADD p (Householder on columns q.., v = d2 + alpha e_q as in qpb_gi.hip)
       const double nrm = nd2 * rsq(nd2);
@@ -249,11 +366,13 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
       wave_lds_sync();
       if (l == q) xch[q] = Dpq + alpha;
       wave_lds_sync();
-      double v[NP];
-      lds_vec(xch, v);
-      const double w = beta * dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return v[j]; });
+      const double w = beta * dot_xch(E, xch);
 #pragma unroll
-      for (int j = 0; j < NP; ++j) E[j] = __builtin_fma(-w, v[j], E[j]);
+      for (int j = 0; j < NP; j += 2) {
+        const double2 v = *reinterpret_cast<const double2 *>(&xch[j]);
+        E[j] = __builtin_fma(-w, v.x, E[j]);
+        E[j + 1] = __builtin_fma(-w, v.y, E[j + 1]);
+      }
       if (l < NP) R[q * NP + l] = (l < q) ? dl : 0.0;
       if (l == q) {
         rdg = alpha;
@@ -264,6 +383,7 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
       if (l == p) act = true;
       ++q;
       selecting = true;
+      clk.tick(7);  // add
     } else {
       // DROP active position k
       const int c = __builtin_amdgcn_readlane(iam, k);
@@ -318,8 +438,10 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
       if (l < q) R[l * NP + l] = 0.0;
       rdg = dg;
       invRd = (l < q) ? rcp(dg) : 0.0;
+      clk.tick(8);  // drop
     }
   }
+  clk.tick(9);  // loop exit
 
   // ------------------------------------------------------------- outputs
   // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iact_k}, then L y = g,
@@ -349,6 +471,7 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
   }
   xl = -xl;
   if (status == QPB_OK && wave_any(l < n && !(__builtin_fabs(xl) < kInf))) status = QPB_NUMERICAL;
+  clk.tick(10);  // x = -H^{-1} (f + A^T lam)
   // lambda scatter through LDS (64 entries over xch + the start of R)
   wave_lds_sync();
   double *lamb = R;
@@ -368,6 +491,8 @@ __global__ __launch_bounds__(64, 2) void gi_wave_kernel(
     statg[g] = status;
     if (itg) itg[g] = it;
   }
+  clk.tick(11);  // stores
+  clk.flush(dbg);
 }
 
 }  // namespace wv
@@ -378,7 +503,20 @@ extern "C" hipError_t qpb_launch_gi_wave(const qpb_desc *d, const double *H, con
                                          int32_t *iters, hipStream_t stream) {
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
-  hipLaunchKernelGGL(qpb::wv::gi_wave_kernel, dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b, x, lam,
+  // two waves per SIMD: at three the 168-VGPR cap spills the sweep (measured
+  // slower, profiles/r01/configs_v2.json)
+  hipLaunchKernelGGL(qpb::wv::gi_wave_kernel<2>, dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b, x, lam,
                      active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t qpb_launch_gi_wave_sections(const qpb_desc *d, const double *H, const double *f,
+                                                  const double *A, const double *b, double *x, double *lam,
+                                                  uint32_t *active, int32_t *status, int32_t *iters,
+                                                  unsigned long long *sections, hipStream_t stream) {
+  const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
+  const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
+  hipLaunchKernelGGL((qpb::wv::gi_wave_kernel<2, true>), dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b,
+                     x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, sections);
   return hipGetLastError();
 }

@@ -114,11 +114,12 @@ def _stream_ptr(stream):
 
 
 def solve(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0, out: Solution | None = None,
-          stream=None) -> Solution:
+          stream=None, flags: int = 0) -> Solution:
     """Batched min 1/2 x^T H x + f^T x s.t. A x <= b on the GPU (torch CUDA float64 tensors).
 
     H (B,n,n), f (B,n), A (B,m,n), b (B,m).  Asynchronous on ``stream``
     (default: torch's current stream).  A/b omitted -> unconstrained solve.
+    ``flags``: QPB_FLAG_DIAG_* kernel variants (measurement only, qpb.h).
     """
     import torch
     if not (H.is_cuda and f.is_cuda):
@@ -138,7 +139,7 @@ def solve(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0, out
                        torch.empty((B, w), dtype=torch.int32, device=dev),
                        torch.empty((B,), dtype=torch.int32, device=dev),
                        torch.empty((B,), dtype=torch.int32, device=dev))
-    d = Desc(n, m, B, max_iter, 0, feas_tol)
+    d = Desc(n, m, B, max_iter, flags, feas_tol)
     rc = _lib.qpb_solve(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(A) if m else None, _ptr(b) if m else None,
                         _ptr(out.x), _ptr(out.lam), _ptr(out.active), _ptr(out.status), _ptr(out.iters),
                         _stream_ptr(stream))
@@ -208,11 +209,14 @@ _lib.qpb_solve_sections.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 11
 _lib.qpb_solve_sections.restype = ctypes.c_int
 SECTION_NAMES = ["load", "cholesky", "substitution", "init", "select", "exchange", "back_solve", "step",
                  "add", "drop", "loop_exit", "output"]
+WAVE_SECTION_NAMES = ["load", "sweep", "init", "select", "exchange", "back_solve", "step", "add", "drop",
+                      "loop_exit", "x", "stores"]
 
 
 def solve_sections(H, f, A, b, sections, *, max_iter: int = 0, out: Solution | None = None, stream=None):
-    """Diagnostic build of the n=16, m=32 kernel: accumulates per-section wave
-    cycles into the int64 CUDA tensor ``sections`` (12 entries)."""
+    """Diagnostic builds of the n=16 (16<m<=32) and 16<n<=32 (m<=64) kernels:
+    accumulate per-section wave ticks (100 MHz) into the int64 CUDA tensor
+    ``sections`` (12 entries: SECTION_NAMES / WAVE_SECTION_NAMES)."""
     import torch
     B, n = f.shape
     m = A.shape[1]

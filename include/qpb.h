@@ -137,10 +137,12 @@ int qpb_ref_solve_host(const qpb_ref_desc *desc, const double *P,
 int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
 		double r, const double *x, double *out, void *stream);
 
-/* Diagnostic: same solve (n = 16, 16 < m <= 32) by a build of the kernel
- * with s_memrealtime stamps (100 MHz); adds each wavefront's ticks per kernel section
- * (12 counters: load, cholesky, substitution, init, select, exchange,
- * back-solve, step, add, drop, loop-exit, output) into sections[]. */
+/* Diagnostic: same solve (n = 16 with 16 < m <= 32, or 16 < n <= 32 with
+ * m <= 64) by a build of the kernel with s_memrealtime stamps (100 MHz); adds
+ * each wavefront's ticks per kernel section into sections[] (12 counters).
+ * n = 16: load, cholesky, substitution, init, select, exchange, back-solve,
+ * step, add, drop, loop-exit, output.  16 < n <= 32: load, sweep, init,
+ * select, exchange, back-solve, step, add, drop, loop-exit, x, stores. */
 int qpb_solve_sections(const qpb_desc *desc, const double *H, const double *f,
 		       const double *A, const double *b, double *x, double *lam,
 		       uint32_t *active, int32_t *status, int32_t *iters,

@@ -33,20 +33,29 @@ def t_kernel(fn, reps=5):
 
 
 def main():
+    # argv: [config names ...] [--flags F]
+    args = sys.argv[1:]
+    flags = 0
+    if "--flags" in args:
+        i = args.index("--flags")
+        flags = int(args[i + 1])
+        del args[i:i + 2]
     out = {}
     for name, n, B, fam, reps in (("c1_n16_m32", 16, 65536, "box", 9), ("c4_n32_m64", 32, 262144, "dense", 5),
                                   ("c3_n128_m256", 128, 16384, "box", 3)):
+        if args and name not in args:
+            continue
         H, f, A, b = qpb.generate(n, B, 20261015, family=fam)
-        sol = qpb.solve(H, f, A, b)
+        sol = qpb.solve(H, f, A, b, flags=flags)
         torch.cuda.synchronize()
         it = sol.iters.double()
-        ms = t_kernel(lambda: qpb.solve(H, f, A, b, out=sol), reps)
-        ms1 = t_kernel(lambda: qpb.solve(H, f, A, b, max_iter=1, out=sol), reps)
+        ms = t_kernel(lambda: qpb.solve(H, f, A, b, out=sol, flags=flags), reps)
+        ms1 = t_kernel(lambda: qpb.solve(H, f, A, b, max_iter=1, out=sol, flags=flags), reps)
         bpq = bench.bytes_per_qp(n, 2 * n)
         out[name] = {"n": n, "m": 2 * n, "batch": B, "family": fam, "kernel_ms": ms, "maxit1_ms": ms1,
                      "qps_per_s": B / (ms * 1e-3), "achieved_GBs": B * bpq / (ms * 1e-3) / 1e9,
                      "frac_of_8TBs": B * bpq / (ms * 1e-3) / 8e12, "iters_mean": float(it.mean()),
-                     "iters_max": int(it.max())}
+                     "iters_max": int(it.max()), "flags": flags}
         print(name, json.dumps(out[name]), file=sys.stderr, flush=True)
     print(json.dumps(out, indent=1))
 
