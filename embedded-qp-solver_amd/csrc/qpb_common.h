@@ -132,6 +132,16 @@ __device__ __forceinline__ double row_min(double v) {
   return v;
 }
 
+// max of a 32-bit key over the 16 lanes of the row: the DPP moves fuse into
+// v_max_u32 (row_ror source modifier), one instruction per step
+__device__ __forceinline__ uint32_t row_max_u32(uint32_t v) {
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 8, 0xF, 0xF, true));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 4, 0xF, 0xF, true));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 2, 0xF, 0xF, true));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 1, 0xF, 0xF, true));
+  return v;
+}
+
 // sum over the 16 lanes of the row by an xor butterfly (quad_perm 1032,
 // quad_perm 2301, row_half_mirror, row_mirror): at every level the two
 // partners add the same two numbers in swapped order, which IEEE addition

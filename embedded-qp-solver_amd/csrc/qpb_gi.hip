@@ -16,7 +16,7 @@
 //           substitution of both D rows of lane l and the lane-parallel y.
 //           Slack of the unconstrained minimiser x0 = -H^{-1} f
 //           (test/qp_ref.py:35's answer): s = b - A x0 = b + D y.
-//   iterate pick the most violated row p (normalised slack, exact row min);
+//   iterate pick the most violated row p (normalised slack, fp32 argmax key);
 //           d = -D[p,:] (= J^T n+ in G-I's notation, J = L^{-T} Q, n+ = -a_p),
 //           dual step r = R^{-1} d1 (lane-parallel back substitution),
 //           partial step t1 (ratio test over the active multipliers),
@@ -138,9 +138,10 @@ __device__ __forceinline__ void gi_group(
   double *gsn = xch + NL;  // Givens sines
 
   // ------------------------------------------------------------------ load
-  // (flags & QPB_FLAG_DIAG_L2: every QP reads the inputs of QP g mod 512 --
-  // a diagnostic that takes HBM latency out of the kernel time)
-  const long long gi = (flags & 1) ? (g & 511) : g;
+  // (flags & QPB_FLAG_DIAG_L2: every QP reads the inputs of QP g mod 512;
+  // QPB_FLAG_DIAG_MALL: of QP g mod 16384 (107 MB, Infinity-Cache resident
+  // after the first launch) -- diagnostics that take HBM out of the kernel time)
+  const long long gi = (flags & 1) ? (g & 511) : (flags & 16) ? (g & 16383) : g;
   const double *Hq = Hg + gi * (long long)n * n;
   // m == 0: A/b may be NULL -- point the (masked) row loads at H instead
   const double *Aq = m > 0 ? Ag + gi * (long long)m * n : Hq;
@@ -339,21 +340,25 @@ __device__ __forceinline__ void gi_group(
   while (!done && it < max_iter) {
     ++it;
     if (selecting) {
-      // most violated row by normalised slack; the key carries the row index
-      double key = kBig;
+      // most violated row by normalised slack.  The violation test is fp64;
+      // the argmax runs on 32-bit keys: the fp32 magnitude of the (negative)
+      // normalised slack with the row index in its low 5 bits, so one
+      // DPP-fused v_max_u32 per step reduces the row (0 = none violated)
+      uint32_t key = 0u;
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const double v = s[r] * invn[r];
         const bool viol = !act[r] && v < thr[r];
-        key = viol ? __builtin_fmin(key, pack_key(v, l + NL * r)) : key;
+        const uint32_t kr = (__float_as_uint((float)(-v)) & ~31u) | (uint32_t)(l + NL * r);
+        key = viol && kr > key ? kr : key;
       }
-      key = row_min(key);
-      if (!(key < 0.0)) {  // no violated row (violations are negative keys)
+      key = row_max_u32(key);
+      if (key == 0u) {
         status = QPB_OK;
         done = true;
         break;
       }
-      p = key_index(key);
+      p = (int)(key & 31u);
       up = 0.0;
       selecting = false;
     }

@@ -85,6 +85,9 @@ typedef enum qpb_error {
 /* diagnostic flag: n = 16, m = 32 by the persistent launch (grid = resident
  * waves, each walks several 4-QP groups and prefetches the next one) */
 #define QPB_FLAG_DIAG_PERSISTENT 8
+/* diagnostic flag (n <= 16): every QP k reads the inputs of QP (k mod 16384),
+ * a 107 MB working set that stays Infinity-Cache resident across launches */
+#define QPB_FLAG_DIAG_MALL 16
 
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""A/B timing of libqpb variants (tools/build_variant.sh) on the same batch,
+rounds interleaved so clock/thermal drift hits every variant alike.
+  python tools/ab.py name1 name2 ...   ('' = lib/libqpb.so)
+env: B (65536), FAM (box), ROUNDS (6), REPS (10)"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import qpb  # noqa: E402
+
+
+def main(names):
+    dev = torch.device("cuda", 0)
+    B = int(os.environ.get("B", 65536))
+    fam = os.environ.get("FAM", "box")
+    rounds, reps = int(os.environ.get("ROUNDS", 6)), int(os.environ.get("REPS", 10))
+    H, f, A, b = bench.make_batch(torch, B, 16, fam, 1, dev)
+    libs = {}
+    for nm in names:
+        path = os.path.join(ROOT, "embedded-qp-solver_amd", "lib", f"libqpb_{nm}.so" if nm else "libqpb.so")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        lib.qpb_solve.argtypes = [ctypes.POINTER(qpb.Desc)] + [ctypes.c_void_p] * 10
+        libs[nm] = lib
+    s = torch.cuda.current_stream()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    sols = {nm: qpb.solve(H, f, A, b) for nm in names}
+    d = qpb.Desc(16, 32, B, 0, 0, 0.0)
+
+    def call(nm):
+        o = sols[nm]
+        rc = libs[nm].qpb_solve(ctypes.byref(d), p(H), p(f), p(A), p(b), p(o.x), p(o.lam), p(o.active), p(o.status),
+                                p(o.iters), ctypes.c_void_p(s.cuda_stream))
+        assert rc == 0, rc
+
+    times = {nm: [] for nm in names}
+    for nm in names:
+        for _ in range(3):
+            call(nm)
+    for _ in range(rounds):
+        for nm in names:
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                call(nm)
+                e1.record(s)
+                e1.synchronize()
+                times[nm].append(e0.elapsed_time(e1) * 1e3)
+    torch.cuda.synchronize()
+    ref = names[0]
+    out = {}
+    for nm in names:
+        t = sorted(times[nm])
+        same = bool(torch.equal(sols[nm].x, sols[ref].x) and torch.equal(sols[nm].active, sols[ref].active))
+        out[nm or "head"] = {"median_us": round(t[len(t) // 2], 1), "min_us": round(t[0], 1),
+                             "same_as_first": same, "iters_mean": float(sols[nm].iters.double().mean())}
+    print(json.dumps({"B": B, "family": fam, "variants": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main([a if a != "head" else "" for a in sys.argv[1:]])
