@@ -290,4 +290,4 @@ extern "C" const char *qpb_last_error(void) { return g_err; }
 
 // the hot kernel revision is part of the string: profiles/pmc_traffic.json is
 // only trusted for the revision it was measured on (bench.py)
-extern "C" const char *qpb_version(void) { return "qpb 0.2 (gfx950; gi_dense v6: fused sweep, one-trip loads, fused reciprocals, 3 waves/SIMD)"; }
+extern "C" const char *qpb_version(void) { return "qpb 0.2 (gfx950; gi_dense v7: fused sweep, one-trip loads, fp32-key select, one-Newton reciprocals, 3 waves/SIMD)"; }

@@ -67,6 +67,8 @@ constexpr int OFF_XCH = OFF_R + NL * NL;  // 392: exchange row d (16), s_p, |d|^
                                           // cos / sin (16 + 16); y / x capture; lambda scatter
 constexpr int SLOT = OFF_XCH + 32;        // 424
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
+// reciprocals and inverse square roots: hardware estimate + one Newton step
+// (rcp1 / rsq1, qpb_common.h)
 static_assert(SLOT % 2 == 0 && OFF_R % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
 static_assert(NL * RS <= SLOT - OFF_R, "input transposes are staged in R + xch");
 
@@ -226,7 +228,7 @@ __device__ __forceinline__ void gi_group(
     const bool ok = FULL || row < m;
     const double nrm2 = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
     bl[r] = ok ? bv[r] : 0.0;
-    invn[r] = nrm2 > 0.0 ? rsq(nrm2) : 0.0;
+    invn[r] = nrm2 > 0.0 ? rsq1(nrm2) : 0.0;
     // violation threshold of the normalised slack (-inf: zero row, never selected)
     thr[r] = nrm2 > 0.0 ? -feas_tol * (1.0 + __builtin_fabs(bl[r]) * invn[r]) : -kInf;
     // a zero row is the constant constraint 0 <= b
@@ -253,7 +255,7 @@ __device__ __forceinline__ void gi_group(
     unroll<NL - k>([&](auto J) { pr[k + J] = bc<k>(Lr[k + J]); });
     const double akk = pr[k];
     spd = spd && (akk > 0.0);
-    const double ik = rsq(akk);
+    const double ik = rsq1(akk);
     const double ik2 = ik * ik;
     const double c = Lr[k] * ik2;
     unroll<NL - 1 - k>([&](auto J) {
@@ -409,11 +411,11 @@ __device__ __forceinline__ void gi_group(
     double t1 = kBig;
     int k = 0;
     if (qmax > 0) {
-      const double tk = row_min((l < q && rm > 0.0) ? pack_key(um * rcp(rm), l) : kBig);
+      const double tk = row_min((l < q && rm > 0.0) ? pack_key(um * rcp1(rm), l) : kBig);
       t1 = tk;
       k = key_index(tk);
     }
-    const double ir = rsq(nd2);  // 1/|d2| (only used when nd2 > 0)
+    const double ir = rsq1(nd2);  // 1/|d2| (only used when nd2 > 0)
     const double t2 = (nd2 > kDepTol * dd) ? -sp * (ir * ir) : kBig;
     const double t = t1 < t2 ? t1 : t2;
     if (!(t < kBig)) {
@@ -439,7 +441,7 @@ __device__ __forceinline__ void gi_group(
       // nd2 + alpha D[p,q] = |d2| (|d2| + |D[p,q]|): one reciprocal
       const double nrm = nd2 * ir;
       const double alpha = Dpq <= 0.0 ? -nrm : nrm;
-      const double beta = ir * rcp(nrm + __builtin_fabs(Dpq));
+      const double beta = ir * rcp1(nrm + __builtin_fabs(Dpq));
       if (l == q) xch[q] = Dpq + alpha;
       wave_lds_sync();
       double v[NL];
@@ -500,7 +502,7 @@ __device__ __forceinline__ void gi_group(
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
         const double a = R[j * NL + j], bb = R[j * NL + j + 1];
-        const double ir = rsq(__builtin_fma(a, a, bb * bb));
+        const double ir = rsq1(__builtin_fma(a, a, bb * bb));
         const double cj = a * ir, sj = bb * ir;
         const double rj = R[l * NL + j], rj1 = R[l * NL + j + 1];
         wave_lds_sync();
@@ -532,7 +534,7 @@ __device__ __forceinline__ void gi_group(
       wave_lds_sync();
       if (l < q) R[l * NL + l] = 0.0;
       rdg = dg;
-      invRd = (l < q) ? rcp(dg) : 0.0;
+      invRd = (l < q) ? rcp1(dg) : 0.0;
       clk.tick(9);
     }
     wave_lds_sync();
@@ -566,7 +568,7 @@ __device__ __forceinline__ void gi_group(
       });
     });
   }
-  const double invd = rcp(Lp[lrow(l) + l]);
+  const double invd = rcp1(Lp[lrow(l) + l]);
   double Lrow[NL];  // row l of L (entries past l are dead)
 #pragma unroll
   for (int j = 0; j < NL; ++j) Lrow[j] = Lp[lrow(l) + j];

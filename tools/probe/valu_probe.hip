@@ -61,6 +61,24 @@ __global__ __launch_bounds__(64) void lat_kernel(double *out, double seed, long 
   if (threadIdx.x == 0 && blockIdx.x == 0) clk[0] = t1 - t0;
 }
 
+// accuracy of the raw hardware estimates v_rcp_f64 / v_rsq_f64 (relative to
+// IEEE division / sqrt) over inputs spread across many binades
+__global__ void acc_kernel(double *err) {
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long z = 0x9E3779B97F4A7C15ull * (t + 1);
+  double er = 0.0, es = 0.0;
+  for (int i = 0; i < 256; ++i) {
+    z ^= z >> 33; z *= 0xff51afd7ed558ccdull; z ^= z >> 33;
+    const double m = 1.0 + (double)(z >> 12) * 0x1p-52;
+    const double x = __builtin_ldexp(m, (int)((z >> 3) % 200) - 100);
+    const double r = __builtin_amdgcn_rcp(x), q = __builtin_amdgcn_rsq(x);
+    er = fmax(er, fabs(r * x - 1.0));
+    es = fmax(es, fabs(q * sqrt(x) - 1.0));
+  }
+  atomicMax((unsigned long long *)&err[0], __double_as_longlong(er));
+  atomicMax((unsigned long long *)&err[1], __double_as_longlong(es));
+}
+
 int main() {
   double *out;
   long long *clk;
@@ -105,5 +123,13 @@ int main() {
   lat(lat_kernel<2>, ln[2]);
   lat(lat_kernel<3>, ln[3]);
   lat(lat_kernel<4>, ln[4]);
+  double *err;
+  hipMalloc(&err, 2 * sizeof(double));
+  hipMemset(err, 0, 2 * sizeof(double));
+  hipLaunchKernelGGL(acc_kernel, dim3(4096), dim3(256), 0, 0, err);
+  double he[2];
+  hipMemcpy(he, err, sizeof he, hipMemcpyDeviceToHost);
+  printf("{\"probe\": \"accuracy\", \"rcp_f64_max_rel_err\": %.3e, \"rsq_f64_max_rel_err\": %.3e, \"log2\": [%.2f, %.2f]}\n",
+         he[0], he[1], log2(he[0]), log2(he[1]));
   return 0;
 }
