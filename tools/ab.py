@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of libqpb variants (tools/build_variant.sh) on the same batch,
 rounds interleaved so clock/thermal drift hits every variant alike.
-  python tools/ab.py name1 name2 ...   ('' = lib/libqpb.so)
+  python tools/ab.py name1 name2 ...   ('head' = lib/libqpb.so; name@flags adds qpb_desc.flags)
 env: B (65536), FAM (box), ROUNDS (6), REPS (10)"""
 import ctypes
 import json
@@ -23,19 +23,20 @@ def main(names):
     fam = os.environ.get("FAM", "box")
     rounds, reps = int(os.environ.get("ROUNDS", 6)), int(os.environ.get("REPS", 10))
     H, f, A, b = bench.make_batch(torch, B, 16, fam, 1, dev)
-    libs = {}
+    libs, fl = {}, {}
     for nm in names:
-        path = os.path.join(ROOT, "embedded-qp-solver_amd", "lib", f"libqpb_{nm}.so" if nm else "libqpb.so")
+        base, _, fs = nm.partition("@")  # name@flags: the same library with qpb_desc.flags
+        fl[nm] = int(fs or 0)
+        path = os.path.join(ROOT, "embedded-qp-solver_amd", "lib", f"libqpb_{base}.so" if base else "libqpb.so")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         lib.qpb_solve.argtypes = [ctypes.POINTER(qpb.Desc)] + [ctypes.c_void_p] * 10
         libs[nm] = lib
     s = torch.cuda.current_stream()
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     sols = {nm: qpb.solve(H, f, A, b) for nm in names}
-    d = qpb.Desc(16, 32, B, 0, 0, 0.0)
-
     def call(nm):
         o = sols[nm]
+        d = qpb.Desc(16, 32, B, 0, fl[nm], 0.0)
         rc = libs[nm].qpb_solve(ctypes.byref(d), p(H), p(f), p(A), p(b), p(o.x), p(o.lam), p(o.active), p(o.status),
                                 p(o.iters), ctypes.c_void_p(s.cuda_stream))
         assert rc == 0, rc
@@ -65,4 +66,4 @@ def main(names):
 
 
 if __name__ == "__main__":
-    main([a if a != "head" else "" for a in sys.argv[1:]])
+    main([a.replace("head", "", 1) if a.startswith("head") else a for a in sys.argv[1:]])
