@@ -426,6 +426,9 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
             const double e0 = E[jj], e1 = E[jj + 1];
             E[jj] = __builtin_fma(cj, e0, sj * e1);
             E[jj + 1] = __builtin_fma(-sj, e0, cj * e1);
+            // keeps the 31 branches distinct: merged, they would address E
+            // through a pointer phi and put it on the stack (scratch)
+            asm volatile("; rot %0" ::"n"(jj));
           }
         });
       }
