@@ -1,30 +1,42 @@
 #!/usr/bin/env python3
 """bench.py -- QPs/sec of the batched MI355X QP solver (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): per GPU a batch of 65,536 dense QPs,
-n=16, m=32, fp64, solved by the active-set kernel (qpb_solve) through the
-C-ABI.  Synthetic "conditioned box" family: H = B^T B/(1e3 n)
-+ I (the reference generator's P, matrix_ops.c:699-734, shifted), f ~
-U[-1e3,1e3], box |x_i| <= 10 written as a dense A = [I; -I], b = 10 (so the
-solver reads the full dense (H, f, A, b)).  Inputs are generated on the GPU
-and resident in HBM before the timed region.
+Metric (BASELINE.json): "QPs/sec (whole node) at n=16,m=32 batch=1M".  The
+default workload is that config: a GLOBAL batch of 1,048,576 dense QPs, n=16,
+m=32, fp64, sharded by QP index over the ranks (configs[2]; on one GPU it is
+the whole 1 M batch -- 7.26 GB, it fits one MI355X), solved by the active-set
+kernel (qpb_solve) through the C-ABI.  Synthetic "conditioned box" family
+(SURVEY.md §8d): H = B^T B/(1e3 n) + I (the reference generator's P,
+matrix_ops.c:699-734, shifted), f ~ U[-1e3,1e3], box |x_i| <= 10 written as a
+dense A = [I; -I], b = 10 (so the solver reads the full dense (H, f, A, b)).
+Inputs are generated on the GPU and resident in HBM before the timed region.
+This replaces the reference's serial per-QP loop (main.c:36-59).
 
-One step = one qpb_solve launch over the rank's batch.  Multi-GPU: one process
-per GPU (torchrun), QPs sharded by index, no collective in the data path
-(weak scaling); timings are max-reduced over ranks.
+One step = one qpb_solve call over the rank's shard.  Multi-GPU: one process
+per GPU.  `--gpus N` without a torchrun environment relaunches this script
+under torch.distributed.run (a child process, started before anything here
+touches the GPU); every rank solves its contiguous shard with no collective in
+the data path; timings are max-reduced over ranks.  Scaling is "strong": the
+1 M batch is fixed as N grows (`--batch B` gives weak scaling at B per GPU).
 
 Also reported:
   roofline     -- algorithmic HBM bytes per launch / mean kernel time (HIP
                   events on the launch stream) vs 8 TB/s
   cpu_baseline -- the reference's own qp_solvers.c admm() (compiled from
                   /root/reference by oracle/Makefile, box +-10 compiled in) on
-                  a sample of the same QPs, one process per core, rank 0, N=1
+                  a sample of the same QPs, one forked process per core of
+                  this process's CPU share, rank 0, N=1
+  like_for_like -- the reference's Newton and ADMM: the GPU replicas
+                  (qpb_ref_solve) against the compiled reference on the
+                  same QPs (extra keys; N=1 only)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
 
 BASELINE_METRIC = "QPs/sec (whole node) at n=16,m=32 batch=1M; % HBM roofline at 1/2/4/8 GPUs"  # BASELINE.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
+METRIC_BATCH = 1 << 20
 
 
 def bytes_per_qp(n: int, m: int) -> int:
@@ -41,22 +54,14 @@ def bytes_per_qp(n: int, m: int) -> int:
     return 8 * (n * n + n + m * n + m) + 8 * (n + m) + 4 * ((m + 31) // 32) + 4
 
 
-def make_batch(torch, B: int, n: int, family: str, seed: int, device, first: int = 0, box: float = 10.0):
-    """QPs [first, first + B) of the benchmark family, generated on the GPU by
-    qpb_generate (Philox keyed by (seed, QP index): a shard is the same QPs as
-    the matching slice of one big batch)."""
-    import qpb
-    return qpb.generate(n, B, seed, family=family, first=first, shift=1.0, box=box, device=device)
-
-
 def baseline_config(n: int, total: int, world: int) -> str:
-    """Which BASELINE.json config a run measures (configs[1] is the headline)."""
+    """Which BASELINE.json config a run measures."""
+    if n == 16 and total == METRIC_BATCH:
+        return "BASELINE configs[2] (the metric's 1M batch)"
     if n == 16 and total == 65536 and world == 1:
         return "BASELINE configs[1]"
-    if n == 16 and total == 1048576:
-        return "BASELINE configs[2]"
     if n == 32 and total == 262144:
-        return "BASELINE configs[4] shape, fp64 throughout"
+        return "BASELINE configs[4] shape"
     if n == 128 and total == 16384:
         return "BASELINE configs[3]"
     return "not a BASELINE config"
@@ -79,9 +84,26 @@ def pmc_traffic(n: int, m: int, B: int, family: str, library: str):
     return {"bytes": t["hbm_bytes_per_launch"], "source": t.get("source", path)}
 
 
+# --------------------------------------------------------------------------- CPU share
+def cpu_share() -> int:
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU quota
+    and by the OMP_NUM_THREADS share the GPU box sets (16 per GPU there)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 # --------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
-    lib_path, P, q, seconds, iters = args
+    lib_path, fn, P, q, iters, seconds = args
     import ctypes
 
     import numpy as np
@@ -89,14 +111,12 @@ def _cpu_worker(args):
     dp = ctypes.POINTER(ctypes.c_double)
     x0 = np.zeros_like(q)
     x = np.zeros_like(q)
-    done = 0
-    chunk = 64
+    done, chunk, i = 0, 64, 0
     t0 = time.perf_counter()
-    i = 0
     while True:
         j = min(i + chunk, len(q))
-        L.ref_admm_batch(ctypes.c_uint(j - i), P[i:j].ctypes.data_as(dp), q[i:j].ctypes.data_as(dp),
-                         x0[i:j].ctypes.data_as(dp), ctypes.c_uint(iters), x[i:j].ctypes.data_as(dp))
+        getattr(L, fn)(ctypes.c_uint(j - i), P[i:j].ctypes.data_as(dp), q[i:j].ctypes.data_as(dp),
+                       x0[i:j].ctypes.data_as(dp), ctypes.c_uint(iters), x[i:j].ctypes.data_as(dp))
         done += j - i
         i = 0 if j >= len(q) else j
         el = time.perf_counter() - t0
@@ -104,72 +124,105 @@ def _cpu_worker(args):
             return done, el
 
 
-def cpu_baseline(H, f, seconds: float, procs: int):
-    """The reference admm() on the same box QPs (uniform box 10 compiled in,
-    config.h:29-30), one forked process per core (the reference is not
-    thread-safe: static pools kmalloc.c:37-42)."""
+def cpu_run(fn: str, iters: int, H, f, seconds: float, procs: int):
+    """The compiled reference solver `fn` (oracle/ref_driver.c over the
+    unmodified qp_solvers.c) on the given QPs, one forked process per CPU
+    (the reference is not thread-safe: static pools kmalloc.c:37-42)."""
     import multiprocessing as mp
 
     import numpy as np
     lib = os.path.join(ROOT, "oracle", "_ref", "libqpref_n16_10.so")
     if not os.path.exists(lib):
-        return {"value": None, "unit": "QPs/s", "cores": 0, "kind": "reference",
-                "sample": "oracle/_ref/libqpref_n16_10.so missing (build with make -C oracle ref)"}
-    P = np.ascontiguousarray(H)
-    q = np.ascontiguousarray(f)
+        return None
+    P, q = np.ascontiguousarray(H), np.ascontiguousarray(f)
     per = max(1, len(q) // procs)
-    jobs = [(lib, P[k * per:(k + 1) * per], q[k * per:(k + 1) * per], seconds, 10000) for k in range(procs)]
-    ctx = mp.get_context("fork")
-    with ctx.Pool(procs) as pool:
+    jobs = [(lib, fn, P[k * per:(k + 1) * per], q[k * per:(k + 1) * per], iters, seconds) for k in range(procs)]
+    with mp.get_context("fork").Pool(procs) as pool:
         res = pool.map(_cpu_worker, jobs)
-    rate = sum(d / el for d, el in res)
+    return sum(d / el for d, el in res)
+
+
+def cpu_baselines(H, f, seconds: float, procs: int):
+    """cpu_baseline (reference admm(), the reference's only constrained
+    solver) plus the reference Newton for the like-for-like rows."""
+    lib = os.path.join(ROOT, "oracle", "_ref", "libqpref_n16_10.so")
+    if not os.path.exists(lib):
+        return ({"value": None, "unit": "QPs/s", "cores": 0, "kind": "reference",
+                 "sample": "oracle/_ref/libqpref_n16_10.so missing (build with make -C oracle ref)"}, None)
+    admm = cpu_run("ref_admm_batch", 10000, H, f, seconds, procs)
+    newton = cpu_run("ref_newton_batch", 10, H, f, seconds / 2, procs)
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:  # noqa: BLE001
         model = "unknown"
-    return {"value": rate, "unit": "QPs/s", "cores": procs, "kind": "reference",
+    host = os.cpu_count() or procs
+    base = {"value": admm, "unit": "QPs/s", "cores": procs, "kind": "reference",
             "solver": "qp_solvers.c admm() (the reference's only constrained solver), box +-10 compiled in, "
-                      "ADMM_ITERATIONS 1e4",
-            "sample": f"the batch's first {len(q)} QPs (restated on the CPU) cycled for {seconds:.0f} s per process, "
-                      f"{procs} forked processes",
-            "cpu_model": model}
+                      "ADMM_ITERATIONS 1e4 (config.h:38)",
+            "sample": f"the batch's first {len(f)} QPs (restated on the CPU) cycled for {seconds:.0f} s per "
+                      f"process, {procs} forked processes = this process's CPU share",
+            "cpu_model": model, "host_cpus": host,
+            "per_core": admm / procs,
+            "host_extrapolated": admm / procs * host,
+            "host_extrapolated_note": f"per-core rate x all {host} host CPUs (linear; not measured: the "
+                                      f"GPU box grants {procs} CPUs to this job)"}
+    return base, newton
+
+
+# --------------------------------------------------------------------------- multi-GPU launch
+def relaunch(n: int) -> int:
+    """`--gpus N` outside torchrun: run this script under torch.distributed.run
+    as a child process (nothing here has touched the GPU) and return its code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 # --------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="QPs per GPU (weak scaling)")
-    ap.add_argument("--global-batch", type=int, default=0,
-                    help="total QPs sharded over the GPUs (strong scaling; overrides --batch)")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--global-batch", type=int, default=METRIC_BATCH,
+                    help="total QPs sharded over the GPUs (strong scaling; default: the metric's 1M)")
+    ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (weak scaling; overrides --global-batch)")
     ap.add_argument("--gather", action="store_true",
                     help="after the timed region, all-gather x/lam/active/status over RCCL and time it")
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--family", choices=["box", "dense"], default="box")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = this process's CPU share")
     ap.add_argument("--cpu-sample", type=int, default=4096)
+    ap.add_argument("--ref-batch", type=int, default=65536, help="QPs for the GPU Newton/ADMM replica rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify statuses after the timed region")
     args = ap.parse_args()
 
-    import torch
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+
+    import torch
     # CPU baseline first: its worker processes are forked, which is only safe
     # before this process initialises the GPU.  The sample is the first
     # cpu_sample QPs of the GPU batch, restated on the CPU (oracle.family_generate).
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.family == "box":
-        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+    cpu, cpu_newton = None, None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.family == "box" and args.n == 16:
+        procs = args.cpu_procs or cpu_share()
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # CPU restatement of qpb_generate: the first QPs of the GPU batch
         Hc, fc, _, _ = oracle.family_generate(args.n, args.cpu_sample, args.seed, "box")
-        cpu = cpu_baseline(Hc, fc, args.cpu_seconds, procs)
+        cpu, cpu_newton = cpu_baselines(Hc, fc, args.cpu_seconds, procs)
         del Hc, fc
     # one GPU per rank; QPB_DIST_BACKEND=gloo (with ranks sharing a card) rehearses
     # the N>1 path on a one-GPU box -- the driver's runs use RCCL ("nccl")
@@ -189,13 +242,17 @@ def main():
     from qpb.dist import gather_results, max_over_ranks, shard
 
     n, m = args.n, 2 * args.n
-    if args.global_batch:
-        start, B = shard(args.global_batch, rank, world)
-    else:
+    if args.batch:
         start, B = rank * args.batch, args.batch
-    # rank r owns QP indices [r*B, (r+1)*B): its own RNG stream
-    H, f, A, b = make_batch(torch, B, n, args.family, args.seed, device, first=start)
-    sol = qpb.solve(H, f, A, b)  # allocate outputs once
+        total_B = args.batch * world
+    else:
+        total_B = args.global_batch
+        start, B = shard(total_B, rank, world)
+    # rank r owns QP indices [start, start + B): the same QPs as that slice of
+    # a one-GPU run (Philox keyed by the global QP index)
+    H, f, A, b = qpb.generate(n, B, args.seed, family=args.family, first=start, shift=1.0, box=10.0, device=device)
+    stream = torch.cuda.current_stream()
+    sol = qpb.solve(H, f, A, b, stream=stream)  # allocate outputs once
     torch.cuda.synchronize()
 
     def barrier():
@@ -204,14 +261,14 @@ def main():
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        qpb.solve(H, f, A, b, out=sol)
-    stream = torch.cuda.current_stream()
+        qpb.solve(H, f, A, b, out=sol, stream=stream)
+    # HIP events on the stream the kernel is launched on
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
         evs[k][0].record(stream)
-        qpb.solve(H, f, A, b, out=sol)
+        qpb.solve(H, f, A, b, out=sol, stream=stream)
         evs[k][1].record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -221,8 +278,7 @@ def main():
     if args.gather and world > 1:  # the trivial result gather of SURVEY.md §8e, outside the timed steps
         barrier()
         tg = time.perf_counter()
-        full = gather_results({"x": sol.x, "lam": sol.lam, "active": sol.active, "status": sol.status},
-                              args.global_batch or B * world)
+        full = gather_results({"x": sol.x, "lam": sol.lam, "active": sol.active, "status": sol.status}, total_B)
         barrier()
         gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, device)
         del full
@@ -233,12 +289,31 @@ def main():
     if args.check:
         assert ok_frac == 1.0, torch.bincount(st.long())
 
-    total_B = args.global_batch or B * world
+    # like-for-like rows (N = 1): the reference's Newton and ADMM as GPU replicas
+    like = None
+    if rank == 0 and world == 1 and n == 16 and args.family == "box" and args.ref_batch > 0:
+        Br = min(args.ref_batch, B)
+        x0 = torch.zeros((Br, n), dtype=torch.float64, device=device)
+        like = {"qps": Br, "inputs": "the first QPs of the bench batch (P = H, q = f), x0 = 0, ADMM box +-10"}
+        for name, mode, iters in (("newton", qpb.REF_NEWTON, 10), ("admm", qpb.REF_ADMM, 10000)):
+            qpb.ref_solve(mode, H[:Br], f[:Br], x0, iterations=iters, box=(-10.0, 10.0), stream=stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            qpb.ref_solve(mode, H[:Br], f[:Br], x0, iterations=iters, box=(-10.0, 10.0), stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            gpu_rate = Br / (e0.elapsed_time(e1) * 1e-3)
+            cpu_rate = (cpu or {}).get("value") if name == "admm" else cpu_newton
+            like[name] = {"gpu_qps_per_s": gpu_rate, "cpu_reference_qps_per_s": cpu_rate,
+                          "iterations_arg": iters,
+                          "ratio": (gpu_rate / cpu_rate) if cpu_rate else None}
+        if cpu:
+            like["cpu_cores"] = cpu["cores"]
+
     total_qps = total_B * args.steps
     value = total_qps / elapsed
     bpq = bytes_per_qp(n, m)
     achieved = B * bpq / (kern_ms * 1e-3) / 1e9
-
     traffic = pmc_traffic(n, m, B, args.family, qpb.version())
 
     if rank == 0:
@@ -251,25 +326,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.global_batch else "weak",
+            "scaling": "weak" if args.batch else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": f"synthetic: qpb_generate on the GPU (Philox keyed by QP index, seed {args.seed}), "
                     f"conditioned {args.family} family of SURVEY.md §8d",
             "config": {"workload": f"batched active-set QP solve, n={n}, m={m} "
                                    f"({'box as dense A=[I;-I]' if args.family == 'box' else 'dense random A'}), "
-                                   f"{B} QPs per GPU ({baseline_config(n, total_B, world)})",
+                                   f"{total_B} QPs in total, {B} per GPU ({baseline_config(n, total_B, world)})",
                        "n": n, "m": m, "batch_per_gpu": B, "global_batch": total_B,
                        "family": args.family, "parallelism": f"qp-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": ("qpb::gi_dense_kernel<2, true, true, false, 3>" if n <= 16 and m <= 32
+                         "kernel": ("qpb::gi_dense_kernel" if n <= 16 and m <= 32
                                     else "qpb::wv::gi_wave_kernel" if n <= 32 and m <= 64
                                     else "qpb::blk::gi_block_kernel"), "bytes_per_qp": bpq,
-                         "kernel_ms": kern_ms},
+                         "bytes_per_launch": B * bpq, "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
+            "like_for_like": like,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
             "gather_ms": gather_ms,
             "library": qpb.version(),

@@ -58,11 +58,29 @@ static int hip_fail(hipError_t e, const char *what) {
   return fail(QPB_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
 
+// The device census is taken once per process (a HIP runtime query per solve
+// cost ~8 us of host time on every launch); a process without a device keeps
+// failing with QPB_ERR_NO_DEVICE.
+static int device_census(void) {
+  static const int count = [] {
+    int c = 0;
+    return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+  }();
+  return count;
+}
+
 static int check_device(void) {
-  int count = 0;
-  hipError_t e = hipGetDeviceCount(&count);
-  if (e != hipSuccess || count <= 0) return fail(QPB_ERR_NO_DEVICE, "no HIP device available");
+  if (device_census() <= 0) return fail(QPB_ERR_NO_DEVICE, "no HIP device available");
   return 0;
+}
+
+// QPs per launch: a launch's grid holds at most 2^32 - 1 work-items, so each
+// kernel family takes at most 2^32 / (threads per QP) QPs per launch (minus a
+// margin); larger batches are split into consecutive launches on the stream.
+static long long chunk_qps(int n, int m) {
+  if (n <= 16 && m <= 32) return 1LL << 27;  // 16 lanes per QP
+  if (n <= 32 && m <= 64) return 1LL << 25;  // 64 lanes per QP
+  return 1LL << 21;                          // 1024 lanes per QP
 }
 
 static int check_desc(const qpb_desc *d) {
@@ -72,7 +90,6 @@ static int check_desc(const qpb_desc *d) {
   if (d->n > QPB_MAX_N || d->m > QPB_MAX_M)
     return fail(QPB_ERR_UNSUPPORTED, "n=%d m=%d outside this build's kernels (n<=%d, m<=%d)", d->n, d->m,
                 QPB_MAX_N, QPB_MAX_M);
-  if (d->batch > 0x7fffffffLL * 16) return fail(QPB_ERR_UNSUPPORTED, "batch too large for one launch");
   return 0;
 }
 
@@ -89,14 +106,24 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
   if (rc) return rc;
   // n <= 16, m <= 32: four QPs per wavefront; n <= 32, m <= 64: one QP per
   // wavefront; larger: one QP per workgroup
-  hipError_t e;
-  if (d->n <= 16 && d->m <= 32)
-    e = qpb_launch_gi(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
-  else if (d->n <= 32 && d->m <= 64)
-    e = qpb_launch_gi_wave(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
-  else
-    e = qpb_launch_gi_block(d, H, f, A, b, x, lam, active, status, iters, (hipStream_t)stream);
-  if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
+  const long long n = d->n, m = d->m, w = (m + 31) / 32, step = chunk_qps(d->n, d->m);
+  for (long long k0 = 0; k0 < d->batch; k0 += step) {
+    qpb_desc c = *d;
+    c.batch = d->batch - k0 < step ? d->batch - k0 : step;
+    const double *Hc = H + k0 * n * n, *fc = f + k0 * n;
+    const double *Ac = m ? A + k0 * m * n : A, *bc = m ? b + k0 * m : b;
+    double *xc = x + k0 * n, *lc = m ? lam + k0 * m : lam;
+    uint32_t *ac = m ? active + k0 * w : active;
+    int32_t *sc = status + k0, *ic = iters ? iters + k0 : iters;
+    hipError_t e;
+    if (d->n <= 16 && d->m <= 32)
+      e = qpb_launch_gi(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
+    else if (d->n <= 32 && d->m <= 64)
+      e = qpb_launch_gi_wave(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
+    else
+      e = qpb_launch_gi_block(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
+  }
   return 0;
 }
 
@@ -184,7 +211,9 @@ static int check_ref(const qpb_ref_desc *d) {
   if (d->batch < 0 || d->n < 1 || d->iterations < 0) return fail(QPB_ERR_INVALID_ARG, "bad n/batch/iterations");
   if (d->mode != QPB_REF_NEWTON && d->mode != QPB_REF_ADMM && d->mode != QPB_REF_GD)
     return fail(QPB_ERR_INVALID_ARG, "unknown ref mode %d", d->mode);
-  if (d->n > 65535) return fail(QPB_ERR_UNSUPPORTED, "n > 65535 (16-bit dimension field, matrix_type.h:14-17)");
+  if (d->n > 64)
+    return fail(QPB_ERR_UNSUPPORTED, "qpb_ref_solve: n=%d > 64 (the replica keeps P, its LU and two scratch "
+                "matrices in one workgroup's LDS)", d->n);
   return 0;
 }
 
@@ -196,8 +225,15 @@ extern "C" int qpb_ref_solve(const qpb_ref_desc *d, const double *P, const doubl
   if (!P || !q || !x || (!x0 && d->mode != QPB_REF_ADMM)) return fail(QPB_ERR_INVALID_ARG, "P, q, x0, x required");
   rc = check_device();
   if (rc) return rc;
-  hipError_t e = qpb_launch_ref(d, P, q, x0, x, iters, (hipStream_t)stream);
-  if (e != hipSuccess) return hip_fail(e, "qpb_ref_solve launch");
+  // one 64-thread workgroup per QP: at most 2^25 QPs per launch
+  const long long n = d->n, step = 1LL << 25;
+  for (long long k0 = 0; k0 < d->batch; k0 += step) {
+    qpb_ref_desc c = *d;
+    c.batch = d->batch - k0 < step ? d->batch - k0 : step;
+    hipError_t e = qpb_launch_ref(&c, P + k0 * n * n, q + k0 * n, x0 ? x0 + k0 * n : x0, x + k0 * n,
+                                  iters ? iters + k0 : iters, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "qpb_ref_solve launch");
+  }
   return 0;
 }
 
@@ -239,7 +275,8 @@ extern "C" int qpb_ref_generate(const qpb_ref_gen_desc *d, double *P, double *q,
   if (!d) return fail(QPB_ERR_INVALID_ARG, "desc is NULL");
   if (d->n < 1 || d->batch < 0) return fail(QPB_ERR_INVALID_ARG, "n must be >= 1 and batch >= 0");
   if (d->n > 64) return fail(QPB_ERR_UNSUPPORTED, "qpb_ref_generate: n=%d > 64", d->n);
-  if (d->batch > 0x7fffffffLL) return fail(QPB_ERR_UNSUPPORTED, "batch too large for one launch");
+  if (d->batch > (1LL << 25))  // one 64-thread workgroup per QP: 2^32 work-items per launch
+    return fail(QPB_ERR_UNSUPPORTED, "batch > 2^25 QPs per generator call (split it with `first`)");
   if (d->batch > 0 && (!P || !q || !x0)) return fail(QPB_ERR_INVALID_ARG, "NULL output pointer");
   int rc = check_device();
   if (rc) return rc;
@@ -258,7 +295,8 @@ extern "C" int qpb_generate(const qpb_gen_desc *d, double *H, double *f, double 
     return fail(QPB_ERR_INVALID_ARG, "the box family has m = 2n (got n=%d m=%d)", d->n, d->m);
   if (d->n > 128) return fail(QPB_ERR_UNSUPPORTED, "qpb_generate: n=%d > 128", d->n);
   if (d->n > 16 && d->m < d->n) return fail(QPB_ERR_UNSUPPORTED, "qpb_generate: n > 16 needs m >= n");
-  if (d->batch > 0x7fffffffLL) return fail(QPB_ERR_UNSUPPORTED, "batch too large for one launch");
+  if (d->batch > (1LL << 25))  // one 64-thread workgroup per QP: 2^32 work-items per launch
+    return fail(QPB_ERR_UNSUPPORTED, "batch > 2^25 QPs per generator call (split it with `first`)");
   if (d->batch > 0 && (!H || !f || !A || !b)) return fail(QPB_ERR_INVALID_ARG, "NULL output pointer");
   int rc = check_device();
   if (rc) return rc;
@@ -290,4 +328,4 @@ extern "C" const char *qpb_last_error(void) { return g_err; }
 
 // the hot kernel revision is part of the string: profiles/pmc_traffic.json is
 // only trusted for the revision it was measured on (bench.py)
-extern "C" const char *qpb_version(void) { return "qpb 0.2 (gfx950; gi_dense v7: fused sweep, one-trip loads, fp32-key select, one-Newton reciprocals, 3 waves/SIMD)"; }
+extern "C" const char *qpb_version(void) { return "qpb 0.3 (gfx950; gi_dense v7r: fused sweep, one-trip loads, fp32-key select, one-Newton reciprocals, 3 waves/SIMD, live ragged rows)"; }

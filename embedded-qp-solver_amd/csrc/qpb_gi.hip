@@ -121,8 +121,13 @@ __device__ __forceinline__ void gi_group(
   SectionClock<STAMP> clk;
   const int l = threadIdx.x & (NL - 1);
   const int slot = threadIdx.x >> 4;
-  const long long g = grp * QPB + slot;
-  if (g >= batch) return;  // whole 16-lane rows leave together (last group only)
+  // Rows past the end of the batch (last group only) do not leave: they replay
+  // the batch's last QP -- same trip count, so they never extend the wave's
+  // loop -- and store nothing.  Every lane of the wave stays live, so the
+  // cross-row reads (wave_max4's readlanes) only ever see real QP state.
+  const long long graw = grp * QPB + slot;
+  const bool live = graw < batch;
+  const long long g = live ? graw : batch - 1;
   if constexpr (FULL) {
     n = NL;
     m = NL * MR;
@@ -365,7 +370,9 @@ __device__ __forceinline__ void gi_group(
       selecting = false;
     }
     clk.tick(4);
-    const int qmax = wave_max4(q);  // wave-uniform bound on the active set size
+    // wave-uniform bound on the active set size (q <= NL always; the clamp
+    // keeps every R column loop inside the QP's slot regardless)
+    const int qmax = __builtin_elementwise_min(wave_max4(q), NL);
 
     // ---- row p of D and s_p to every lane through the exchange row; the
     // active columns are then zeroed in LDS: d2 = D[p, q:] (d = -D[p,:] in
@@ -411,9 +418,13 @@ __device__ __forceinline__ void gi_group(
     double t1 = kBig;
     int k = 0;
     if (qmax > 0) {
-      const double tk = row_min((l < q && rm > 0.0) ? pack_key(um * rcp1(rm), l) : kBig);
-      t1 = tk;
+      // the packed key (low 5 mantissa bits = position) only picks k; the step
+      // itself is lane k's exact ratio
+      const double ratio = um * rcp1(rm);
+      const double tk = row_min((l < q && rm > 0.0) ? pack_key(ratio, l) : kBig);
       k = key_index(tk);
+      const double tx = __shfl(ratio, k, NL);
+      t1 = tk < kBig ? tx : kBig;
     }
     const double ir = rsq1(nd2);  // 1/|d2| (only used when nd2 > 0)
     const double t2 = (nd2 > kDepTol * dd) ? -sp * (ir * ir) : kBig;
@@ -547,7 +558,7 @@ __device__ __forceinline__ void gi_group(
   // L^T x = -y, lane-parallel: step k broadcasts the finished component from
   // lane k; finished lanes keep updating (dead values) and the components are
   // captured by same-address LDS stores.
-  const int qm = wave_max4(q);
+  const int qm = __builtin_elementwise_min(wave_max4(q), NL);
   double gl = fl;
   {
     // all loads first (branch-free: inactive positions read row 0 and carry
@@ -610,9 +621,9 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
     const int row = l + NL * r;
-    if (FULL || row < m) lamg[g * m + row] = lamb[row];
+    if (live && (FULL || row < m)) lamg[g * m + row] = lamb[row];
   }
-  if (N16 || l < n) xg[g * n + l] = xl;
+  if (live && (N16 || l < n)) xg[g * n + l] = xl;
   const int sh = (threadIdx.x & 63) & ~(NL - 1);
   uint32_t w0 = 0;
 #pragma unroll
@@ -620,7 +631,7 @@ __device__ __forceinline__ void gi_group(
     const unsigned long long bal = __ballot(act[r]);
     w0 |= (uint32_t)((bal >> sh) & 0xFFFFull) << (16 * r);
   }
-  if (l == 0) {
+  if (live && l == 0) {
     if (m > 0) actg[g] = w0;
     statg[g] = status;
     if (itg) itg[g] = it;

@@ -285,10 +285,14 @@ __global__ __launch_bounds__(1024, 1) void gi_block_kernel(
       double t1 = kBig;
       int k = 0;
       if (q > 0) {
-        const double k0 = (lane < q && r0 > 0.0) ? pack_key256(um0 / r0, lane) : kBig;
-        const double k1 = (lane + 64 < q && r1 > 0.0) ? pack_key256(um1 / r1, lane + 64) : kBig;
-        t1 = wave_min64(__builtin_fmin(k0, k1));
-        k = key_index256(t1);
+        // the packed keys only pick k; the step is position k's exact ratio
+        const double q0 = um0 / r0, q1 = um1 / r1;
+        const double k0 = (lane < q && r0 > 0.0) ? pack_key256(q0, lane) : kBig;
+        const double k1 = (lane + 64 < q && r1 > 0.0) ? pack_key256(q1, lane + 64) : kBig;
+        const double tk = wave_min64(__builtin_fmin(k0, k1));
+        k = key_index256(tk);
+        const double tx = k < 64 ? readlane_d(q0, k) : readlane_d(q1, k - 64);
+        t1 = tk < kBig ? tx : kBig;
       }
       const double t2 = (nd2 > kDepTol * dd) ? -sp / nd2 : kBig;
       const double t = t1 < t2 ? t1 : t2;

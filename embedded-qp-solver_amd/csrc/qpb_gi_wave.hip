@@ -341,9 +341,12 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     double t1 = kBig;
     int k = 0;
     if (q > 0) {
-      const double tk = wave_min((l < q && rm > 0.0) ? pack_key64(um * rcp(rm), l) : kBig);
-      t1 = tk;
+      // the packed key only picks k; the step is lane k's exact ratio
+      const double ratio = um * rcp(rm);
+      const double tk = wave_min((l < q && rm > 0.0) ? pack_key64(ratio, l) : kBig);
       k = __builtin_amdgcn_readfirstlane(key_index64(tk));
+      const double tx = readlane_d(ratio, k);
+      t1 = tk < kBig ? tx : kBig;
     }
     const double t2 = (nd2 > kDepTol * dd) ? -sp * rcp(nd2) : kBig;
     const double t = t1 < t2 ? t1 : t2;

@@ -25,7 +25,9 @@ def max_over_ranks(value: float, device=None) -> float:
     import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    # RCCL reduces device tensors; gloo (CPU rehearsals) host tensors
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
