@@ -171,6 +171,37 @@ __device__ __forceinline__ double row_sum(double v) {
   return v;
 }
 
+// acc += src[lane K of this 16-lane row] * mul: v_fmac_f64 with a DPP
+// row_newbcast source operand (gfx950's DP ALU DPP), the broadcast fused into
+// the FMA instead of a separate v_mov_b64_dpp.  hipcc neither forms this
+// instruction nor pads hazards inside inline asm: callers guarantee that no
+// VALU instruction wrote `src` in the two instructions before (the VALU-write
+// -> DPP-read hazard), e.g. by an ordering point between the producing step
+// and this one (fmac_bc), or use fmac_bc_nop, which issues the 2 wait states.
+template <int K>
+__device__ __forceinline__ void fmac_bc(double &acc, double src, double mul) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(src), "v"(mul), "i"(K));
+}
+template <int K>
+__device__ __forceinline__ void fmac_bc_nop(double &acc, double src, double mul) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(src), "v"(mul), "i"(K));
+}
+
+// exact min over the 16 lanes of the row (v_min_f64 on row_ror moves)
+__device__ __forceinline__ double row_min_exact(double v) { return row_min(v); }
+// min of a 32-bit value over the 16 lanes of the row (DPP-fused v_min_u32)
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
+  v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 8, 0xF, 0xF, true));
+  v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 4, 0xF, 0xF, true));
+  v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 2, 0xF, 0xF, true));
+  v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 1, 0xF, 0xF, true));
+  return v;
+}
+
 // max of a per-row-uniform int over the 4 rows of the wave, as a wave-uniform
 // (SGPR) value: bounds for skipping dead steps of unrolled loops.
 __device__ __forceinline__ int wave_max4(int v) {

@@ -47,6 +47,26 @@
 #include "qpb_common.h"
 #include "qpb.h"
 
+// A/B switches of the round-2 changes (all on in the shipped build)
+#ifndef QPB_DPPFMA
+#define QPB_DPPFMA 1  // broadcasts fused into v_fmac_f64_dpp (sweep, back substitution)
+#endif
+#ifndef QPB_DDINV
+#define QPB_DDINV 0  // |D[p,:]|^2 from the setup (invariant under the column rotations)
+#endif
+#ifndef QPB_ROWLOAD
+#define QPB_ROWLOAD 0  // each lane loads its own rows (no LDS transposes)
+#endif
+#ifndef QPB_SINC
+#define QPB_SINC 1  // s = b + D y accumulated inside the sweep (no y round trip through LDS)
+#endif
+#ifndef QPB_PF_DIST
+#define QPB_PF_DIST 0  // > 0: each wave prefetches the input lines of group blockIdx + QPB_PF_DIST
+#endif
+#ifndef QPB_RATIO_MIN
+#define QPB_RATIO_MIN 1  // ratio test: exact f64 min + u32 argmin, no LDS round trip
+#endif
+
 namespace qpb {
 
 constexpr int NL = 16;  // lanes per QP
@@ -163,7 +183,44 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
   for (int r = 0; r < MR; ++r) bv[r] = bq[(FULL || l + NL * r < m) ? l + NL * r : 0];
   const double fv = fg[gi * n + (l < n ? l : n - 1)];
-  if constexpr (N16) {
+  if constexpr (N16 && QPB_ROWLOAD) {
+    // Each lane loads the rows it owns -- H row l, A rows l and l + 16 -- as
+    // eight 16-byte pieces each, straight into registers: every 128-B row is
+    // one cache line, read whole by the lane's 8 loads; no LDS transposes.
+    // All loads are issued at once (one HBM round trip); an empty asm
+    // consumes them right here, since instruction selection would otherwise
+    // sink each load to its first use.
+    double2 hv[8], av[MR][8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) hv[t] = *reinterpret_cast<const double2 *>(&Hq[l * NL + 2 * t]);
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+      const int row = l + NL * r;
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        av[r][t] = (FULL || row < m) ? *reinterpret_cast<const double2 *>(&Aq[row * NL + 2 * t])
+                                     : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(bv[r]));
+    asm volatile("" ::"v"(fv));
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      asm volatile("" ::"v"(hv[t].x), "v"(hv[t].y));
+#pragma unroll
+      for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(av[r][t].x), "v"(av[r][t].y));
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      Lr[2 * t] = hv[t].x;
+      Lr[2 * t + 1] = hv[t].y;
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        E[r][2 * t] = av[r][t].x;
+        E[r][2 * t + 1] = av[r][t].y;
+      }
+    }
+  } else if constexpr (N16) {
     // Coalesced 16-byte loads: one instruction reads 2 whole rows (256 B) of
     // each of the wave's 4 QPs -- lane l gets row 2t + (l>>3), columns
     // 2(l&7), 2(l&7)+1.  Rows reach their owner lane through a transpose in
@@ -253,9 +310,39 @@ __device__ __forceinline__ void gi_group(
   // never read); y_k and 1/L_kk are captured by same-address LDS stores.
   bool spd = true;
   double ya = fl;
+#if QPB_SINC
+#pragma unroll
+  for (int r = 0; r < MR; ++r) s[r] = bl[r];
+#endif
   unroll<NL>([&](auto K) {
     constexpr int k = K;
     __builtin_amdgcn_sched_barrier(0);
+#if QPB_DPPFMA
+    // the pivot row is read straight from lane k by the FMAs (v_fmac_f64_dpp);
+    // the sched_barrier above and the rsq chain below keep every write of
+    // Lr[j] (previous step) well over two instructions before these reads.
+    // Lane k's own Lr[j] is updated last, after the D rows have read it.
+    const double akk = bc<k>(Lr[k]);
+    spd = spd && (akk > 0.0);
+    const double ik = rsq1(akk);
+    const double ik2 = ik * ik;
+    const double nc = -(Lr[k] * ik2);
+    double ne2[MR];
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+      const double e = E[r][k];
+      ne2[r] = -(e * ik2);
+      E[r][k] = e * ik;
+    }
+    unroll<NL - 1 - k>([&](auto J) {
+      constexpr int j = k + 1 + J;
+#pragma unroll
+      for (int r = 0; r < MR; ++r) fmac_bc<k>(E[r][j], Lr[j], ne2[r]);
+      fmac_bc<k>(Lr[j], Lr[j], nc);
+    });
+    Lr[k] *= ik;
+    const double c = -nc;
+#else
     double pr[NL];
     unroll<NL - k>([&](auto J) { pr[k + J] = bc<k>(Lr[k + J]); });
     const double akk = pr[k];
@@ -279,9 +366,16 @@ __device__ __forceinline__ void gi_group(
         pin(E[r][j]);
       });
     }
+#endif
     const double fk = bc<k>(ya);
     ya = __builtin_fma(-c, fk, ya);
+#if QPB_SINC
+    const double yk = fk * ik;  // y_k; D[r][k] is final now
+#pragma unroll
+    for (int r = 0; r < MR; ++r) s[r] = __builtin_fma(E[r][k], yk, s[r]);
+#else
     xch[k] = fk * ik;  // y_k
+#endif
   });
   __builtin_amdgcn_sched_barrier(0);
   // L -> LDS, packed rows (lane l writes row l), kept for the final solves.
@@ -293,6 +387,7 @@ __device__ __forceinline__ void gi_group(
     Lp[lrow(l) + j] = Lr[j];
     wave_lds_sync();
   });
+#if !QPB_SINC
   {
     double yv[NL];
     lds_row16(xch, yv);
@@ -301,6 +396,14 @@ __device__ __forceinline__ void gi_group(
       s[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return yv[j]; }, bl[r]);
     }
   }
+#endif
+#if QPB_DDINV
+  // |D[r,:]|^2 = |a_r L^{-T}|^2: the loop's column reflections and rotations
+  // are orthogonal, so it never changes (used by the dependency test)
+  double ddr[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) ddr[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
+#endif
   clk.tick(1);
   clk.tick(2);
 
@@ -384,13 +487,22 @@ __device__ __forceinline__ void gi_group(
         if (r == prow) {
 #pragma unroll
           for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[r][j], E[r][j + 1]);
+#if QPB_DDINV
+          *reinterpret_cast<double2 *>(&xch[NL]) = make_double2(s[r], ddr[r]);
+#else
           xch[NL] = s[r];
+#endif
         }
     }
     wave_lds_sync();
     const double Dpl = xch[l];
     const double Dpq = xch[q];  // q == 16 reads s_p: only used by an ADD, impossible then
+#if QPB_DDINV
+    const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NL]);
+    const double sp = spdd.x, dd = spdd.y;  // s_p, |D[p,:]|^2
+#else
     const double sp = xch[NL];
+#endif
 
     wave_lds_sync();
     if (l < q) xch[l] = 0.0;
@@ -399,18 +511,33 @@ __device__ __forceinline__ void gi_group(
     lds_row16(xch, d2);
     const double dl = -Dpl;  // d1 component of active position l
     const double nd2 = row_sum(l >= q ? Dpl * Dpl : 0.0);  // |d2|^2
+#if !QPB_DDINV
     const double dd = row_sum(Dpl * Dpl);                   // |D[p,:]|^2
+#endif
     clk.tick(5);
 
     // ---- r = R^{-1} d1: lane-parallel back substitution over the active positions
     double rm = 0.0;
     if (qmax > 0) {
+#if QPB_DPPFMA
+      // on the negated accumulator: nacc_l += R[l][j] * r_j, r_j = nacc_j * (-1/R_jj)
+      // read from lane j by the FMA itself (the product was written just
+      // before: fmac_bc_nop issues the DPP read hazard's wait states)
+      const double ninv = -invRd;
+      double nacc = (l < q) ? Dpl : 0.0;  // = -d1_l
+      unroll<NL>([&](auto JJ) {
+        constexpr int j = NL - 1 - JJ;
+        if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, R[j * NL + l]);
+      });
+      rm = nacc * ninv;  // r_l (0 for l >= q)
+#else
       double acc = (l < q) ? dl : 0.0;
       unroll<NL>([&](auto JJ) {
         constexpr int j = NL - 1 - JJ;
         if (j < qmax) acc = __builtin_fma(-R[j * NL + l], bc<j>(acc * invRd), acc);
       });
       rm = acc * invRd;  // r_l (0 for l >= q)
+#endif
     }
     clk.tick(6);
 
@@ -421,10 +548,16 @@ __device__ __forceinline__ void gi_group(
       // the packed key (low 5 mantissa bits = position) only picks k; the step
       // itself is lane k's exact ratio
       const double ratio = um * rcp1(rm);
+#if QPB_RATIO_MIN
+      const bool cand = l < q && rm > 0.0;
+      t1 = row_min(cand ? ratio : kBig);  // exact minimum
+      k = (int)row_min_u32(cand && ratio == t1 ? (uint32_t)l : 31u) & (NL - 1);
+#else
       const double tk = row_min((l < q && rm > 0.0) ? pack_key(ratio, l) : kBig);
       k = key_index(tk);
       const double tx = __shfl(ratio, k, NL);
       t1 = tk < kBig ? tx : kBig;
+#endif
     }
     const double ir = rsq1(nd2);  // 1/|d2| (only used when nd2 > 0)
     const double t2 = (nd2 > kDepTol * dd) ? -sp * (ir * ir) : kBig;
@@ -649,8 +782,16 @@ __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
     long long batch, int max_iter, double feas_tol, int flags = 0,
     unsigned long long *__restrict__ dbg = nullptr) {
   __shared__ double lds[QPB * SLOT];
+  long long nxt = -1;
+  if constexpr (QPB_PF_DIST > 0) {
+    // the group a wave dispatched about one wave lifetime from now will
+    // solve: its lines are pulled into the Infinity Cache while this group
+    // iterates, so that wave's loads hit on-die instead of queueing for HBM
+    const long long ngroups = (batch + QPB - 1) / QPB;
+    nxt = (long long)blockIdx.x + QPB_PF_DIST < ngroups ? (long long)blockIdx.x + QPB_PF_DIST : -1;
+  }
   gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
-                                 flags, dbg, blockIdx.x, -1);
+                                 flags, dbg, blockIdx.x, nxt);
 }
 
 // persistent form: the grid covers the resident waves once; each wave walks

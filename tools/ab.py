@@ -2,7 +2,7 @@
 """A/B timing of libqpb variants (tools/build_variant.sh) on the same batch,
 rounds interleaved so clock/thermal drift hits every variant alike.
   python tools/ab.py name1 name2 ...   ('head' = lib/libqpb.so; name@flags adds qpb_desc.flags)
-env: B (65536), FAM (box), ROUNDS (6), REPS (10)"""
+env: B (1048576), FAM (box), ROUNDS (5), REPS (6)"""
 import ctypes
 import json
 import os
@@ -13,16 +13,15 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
 import torch  # noqa: E402
 
-import bench  # noqa: E402
 import qpb  # noqa: E402
 
 
 def main(names):
     dev = torch.device("cuda", 0)
-    B = int(os.environ.get("B", 65536))
+    B = int(os.environ.get("B", 1 << 20))
     fam = os.environ.get("FAM", "box")
-    rounds, reps = int(os.environ.get("ROUNDS", 6)), int(os.environ.get("REPS", 10))
-    H, f, A, b = bench.make_batch(torch, B, 16, fam, 1, dev)
+    rounds, reps = int(os.environ.get("ROUNDS", 5)), int(os.environ.get("REPS", 6))
+    H, f, A, b = qpb.generate(16, B, 1, family=fam, shift=1.0, box=10.0, device=dev)
     libs, fl = {}, {}
     for nm in names:
         base, _, fs = nm.partition("@")  # name@flags: the same library with qpb_desc.flags

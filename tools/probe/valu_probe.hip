@@ -27,6 +27,16 @@ __global__ __launch_bounds__(64) void thr_kernel(double *out, double seed, long 
       if constexpr (KIND == 3) a[i] = __builtin_amdgcn_mov_dpp(a[i], 0x151, 0xF, 0xF, true);  // row_newbcast:1
       if constexpr (KIND == 4) a[i] = __builtin_amdgcn_mov_dpp(a[i], 0x121, 0xF, 0xF, true);  // row_ror:1
       if constexpr (KIND == 5) a[i] = __builtin_amdgcn_rcp(a[i]);
+      if constexpr (KIND == 6)  // v_fmac_f64 with a row_newbcast DPP source (a[i] written 7 instructions earlier)
+        asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(a[i]) : "v"(a[i]), "v"(0.999));
+      if constexpr (KIND == 7) {  // v_pk_fma_f32 (two fp32 FMAs per lane)
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 v = {fa[i], fa[(i + 1) & 7]};
+        v = __builtin_elementwise_fma(v, (f2){0.999f, 0.999f}, (f2){1e-3f, 1e-3f});
+        fa[i] = v.x; fa[(i + 1) & 7] = v.y;
+      }
+      if constexpr (KIND == 8)  // the unfused pair: v_mov_b64_dpp + v_fmac_f64
+        a[i] = __builtin_fma(__builtin_amdgcn_mov_dpp(a[i], 0x151, 0xF, 0xF, true), 0.999, a[i]);
     }
     asm volatile("" ::: "memory");
   }
@@ -88,7 +98,8 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  const char *tn[] = {"fma_f64", "mul_f64", "fma_f32", "mov_b64_dpp_bcast", "mov_dpp_ror_f64", "rcp_f64"};
+  const char *tn[] = {"fma_f64", "mul_f64", "fma_f32", "mov_b64_dpp_bcast", "mov_dpp_ror_f64", "rcp_f64",
+                      "fmac_f64_dpp_bcast", "pk_fma_f32", "mov_b64_dpp+fma_f64"};
   auto thr = [&](auto kern, const char *name) {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, 0, out, 1.0, clk);
     hipEventRecord(e0);
@@ -109,6 +120,9 @@ int main() {
   thr(thr_kernel<3>, tn[3]);
   thr(thr_kernel<4>, tn[4]);
   thr(thr_kernel<5>, tn[5]);
+  thr(thr_kernel<6>, tn[6]);
+  thr(thr_kernel<7>, tn[7]);
+  thr(thr_kernel<8>, tn[8]);
   const char *ln[] = {"fma_f64_dep", "mov_b64_dpp_dep", "dpp_ror+min_f64_dep", "ds_write+ds_read_f64_dep",
                       "rcp_f64_dep"};
   auto lat = [&](auto kern, const char *name) {
