@@ -24,6 +24,9 @@ extern "C" hipError_t qpb_launch_gi_wave_sections(const qpb_desc *d, const doubl
 extern "C" hipError_t qpb_launch_gi_wave(const qpb_desc *d, const double *H, const double *f, const double *A,
                                          const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
                                          int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_mixed(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                          const double *b, double *x, double *lam, uint32_t *active,
+                                          int32_t *status, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_gi_block(const qpb_desc *d, const double *H, const double *f, const double *A,
                                           const double *b, double *x, double *lam, uint32_t *active,
                                           int32_t *status, int32_t *iters, hipStream_t stream);
@@ -118,6 +121,8 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
     hipError_t e;
     if (d->n <= 16 && d->m <= 32)
       e = qpb_launch_gi(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
+    else if (d->n <= 32 && d->m <= 64 && (d->flags & QPB_FLAG_MIXED))
+      e = qpb_launch_gi_mixed(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
     else if (d->n <= 32 && d->m <= 64)
       e = qpb_launch_gi_wave(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
     else

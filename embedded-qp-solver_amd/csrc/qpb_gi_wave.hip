@@ -84,7 +84,10 @@ __device__ __forceinline__ double dot_xch(const double (&E)[NP], const double *x
 }
 
 // one QP per wavefront; MR = 1 (m <= 64); OCC waves per SIMD
-template <int OCC, bool STAMP = false>
+// REDO: solve only the QPs the mixed-precision kernel marked (status
+// kRedoStatus, qpb_gi_mixed.hip); every other wave exits at once
+constexpr int32_t kRedoStatus = 100;
+template <int OCC, bool STAMP = false, bool REDO = false>
 __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg, uint32_t *__restrict__ actg,
@@ -95,6 +98,9 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   const int l = threadIdx.x;
   const long long g = blockIdx.x;
   if (g >= batch) return;
+  if constexpr (REDO) {
+    if (statg[g] != kRedoStatus) return;
+  }
   double *Lp = lds + OFF_L;
   double *R = lds + OFF_R;
   double *xch = lds + OFF_X;
@@ -524,5 +530,15 @@ extern "C" hipError_t qpb_launch_gi_wave_sections(const qpb_desc *d, const doubl
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
   hipLaunchKernelGGL((qpb::wv::gi_wave_kernel<2, true>), dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b,
                      x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, sections);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t qpb_launch_gi_wave_redo(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                              const double *b, double *x, double *lam, uint32_t *active,
+                                              int32_t *status, int32_t *iters, hipStream_t stream) {
+  const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
+  const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
+  hipLaunchKernelGGL((qpb::wv::gi_wave_kernel<2, false, true>), dim3((unsigned)d->batch), dim3(64), 0, stream, H, f,
+                     A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol);
   return hipGetLastError();
 }

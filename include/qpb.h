@@ -89,6 +89,18 @@ typedef enum qpb_error {
  * a 107 MB working set that stays Infinity-Cache resident across launches */
 #define QPB_FLAG_DIAG_MALL 16
 
+/* n in (16, 32], m <= 64 (BASELINE configs[4]): mixed precision -- the
+ * active set is found in fp32 (factorisation and iterations), then x and lam
+ * are refined in fp64 on the KKT system of that active set (fp32 factors,
+ * fp64 residuals) and verified in fp64 (feasibility of every row, lam >= 0,
+ * converged refinement).  QPs that fail verification are re-solved by the
+ * fp64 kernel in a second launch, so results meet the fp64 path's bars.
+ * Ignored outside that size class. */
+#define QPB_FLAG_MIXED 32
+/* diagnostic flag (with QPB_FLAG_MIXED): skip the fp64 re-solve; QPs that
+ * would be re-solved keep status 100 (measures the re-solve fraction) */
+#define QPB_FLAG_DIAG_NO_REDO 64
+
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */
 	int32_t m;        /* rows of A x <= b, 0..QPB_MAX_M (0: unconstrained) */

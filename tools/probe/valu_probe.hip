@@ -17,6 +17,11 @@ __global__ __launch_bounds__(64) void thr_kernel(double *out, double seed, long 
   float fa[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) fa[i] = (float)a[i];
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 pk[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pk[i] = (f2){fa[i], fa[i] + 1.0f};
+  const f2 pkm = {0.999f, 0.999f}, pka = {1e-3f, 1e-3f};
   const long long t0 = wall_clock64();
   for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
@@ -29,12 +34,8 @@ __global__ __launch_bounds__(64) void thr_kernel(double *out, double seed, long 
       if constexpr (KIND == 5) a[i] = __builtin_amdgcn_rcp(a[i]);
       if constexpr (KIND == 6)  // v_fmac_f64 with a row_newbcast DPP source (a[i] written 7 instructions earlier)
         asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(a[i]) : "v"(a[i]), "v"(0.999));
-      if constexpr (KIND == 7) {  // v_pk_fma_f32 (two fp32 FMAs per lane)
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 v = {fa[i], fa[(i + 1) & 7]};
-        v = __builtin_elementwise_fma(v, (f2){0.999f, 0.999f}, (f2){1e-3f, 1e-3f});
-        fa[i] = v.x; fa[(i + 1) & 7] = v.y;
-      }
+      if constexpr (KIND == 7)  // v_pk_fma_f32 (two fp32 FMAs per lane), 8 independent packed chains
+        asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(pk[i]) : "v"(pkm), "v"(pka));
       if constexpr (KIND == 8)  // the unfused pair: v_mov_b64_dpp + v_fmac_f64
         a[i] = __builtin_fma(__builtin_amdgcn_mov_dpp(a[i], 0x151, 0xF, 0xF, true), 0.999, a[i]);
     }
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(64) void thr_kernel(double *out, double seed, long 
   const long long t1 = wall_clock64();
   double s = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s += a[i] + fa[i];
+  for (int i = 0; i < 8; ++i) s += a[i] + fa[i] + pk[i].x + pk[i].y;
   out[blockIdx.x * 64 + threadIdx.x] = s;
   if (threadIdx.x == 0 && blockIdx.x == 0) clk[0] = t1 - t0;
 }
