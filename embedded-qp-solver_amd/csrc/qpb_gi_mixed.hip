@@ -51,8 +51,14 @@ static_assert(NP * RST <= OFF_X, "load staging fits in L + R");
 static_assert(OFF_D % 4 == 0, "fp64 area 16-byte aligned");
 constexpr float kDepTol32 = 1e-10f;  // |d2|^2 <= kDepTol32 |d|^2  <=>  z = 0 (fp32 noise ~1e-14)
 constexpr float kFeas32 = 1e-6f;     // fp32 violation threshold (relative); fp64 verifies against feas_tol
-constexpr int kRefine = 2;           // fp64 refinement steps
+constexpr int kRefine = 3;           // fp64 refinement steps (at most; stops once converged)
 constexpr int32_t kRedo = 100;       // internal status: re-solve in fp64
+#ifndef QPB_MX_OCC
+#define QPB_MX_OCC 3  // waves per SIMD
+#endif
+#ifndef QPB_MX_STAGE
+#define QPB_MX_STAGE 3  // diagnostic builds: 0 fp32 only, 1 + initial x, 2 + refinement, 3 + verification
+#endif
 
 __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
@@ -93,6 +99,7 @@ __device__ __forceinline__ double wave_maxd(double v) {
   return __builtin_fmax(__builtin_fmax(a, b), __builtin_fmax(c, d));
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
+__device__ __forceinline__ void pinf(float &v) { asm volatile("" : "+v"(v)); }
 // a finite fp32 key whose low 6 mantissa bits carry a lane index
 __device__ __forceinline__ float pack_key64f(float v, int idx) {
   return __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, v) & ~63u) | (uint32_t)idx);
@@ -113,39 +120,27 @@ __device__ __forceinline__ float dot_xchf(const float (&E)[NP], const float *x) 
   return a0 + a1;
 }
 
-// fp64 dot of a global fp64 row (n entries) with the fp64 vector in LDS
+// fp64 dot of a global fp64 row (n entries) with the fp64 vector in LDS;
+// eight loads in flight at a time (all 32 at once would need 64 VGPRs)
 __device__ __forceinline__ double row_dot(const double *__restrict__ row, int n, const double *xd) {
+  asm volatile("" : "+v"(row));  // per-call loads (see at_w)
   double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-  for (int j = 0; j < NP; j += 2) {
-    const double2 xv = *reinterpret_cast<const double2 *>(&xd[j]);
-    if (j < n) a0 = __builtin_fma(row[j], xv.x, a0);
-    if (j + 1 < n) a1 = __builtin_fma(row[j + 1], xv.y, a1);
+  for (int j0 = 0; j0 < NP; j0 += 8) {
+    double r[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) r[t] = row[j0 + t < n ? j0 + t : 0];
+#pragma unroll
+    for (int t = 0; t < 8; t += 2) {
+      const double2 xv = *reinterpret_cast<const double2 *>(&xd[j0 + t]);
+      a0 = __builtin_fma(j0 + t < n ? r[t] : 0.0, xv.x, a0);
+      a1 = __builtin_fma(j0 + t + 1 < n ? r[t + 1] : 0.0, xv.y, a1);
+    }
   }
   return a0 + a1;
 }
 
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
-
-// H^{-1} g = L^{-T} L^{-1} g in fp64 arithmetic with the fp32 L (packed rows
-// in LDS); lane l holds component l (l < n), lanes >= n return 0
-__device__ __forceinline__ double hinv(double g, int n, int l, const float *Lp, double invd) {
-  const int ll = l & (NP - 1);
-  double acc = g, yl = 0.0;
-  for (int kk = 0; kk < n; ++kk) {
-    const double yk = readlane_d(acc * invd, kk);
-    if (l == kk) yl = yk;
-    acc = __builtin_fma(-((ll > kk) ? (double)Lp[lrow(ll) + kk] : 0.0), yk, acc);
-  }
-  acc = yl;
-  double xl = 0.0;
-  for (int kk = n - 1; kk >= 0; --kk) {
-    const double xk = readlane_d(acc * invd, kk);
-    if (l == kk) xl = xk;
-    acc = __builtin_fma(-((ll < kk) ? (double)Lp[lrow(kk) + ll] : 0.0), xk, acc);
-  }
-  return l < n ? xl : 0.0;
-}
 
 // (R^T R)^{-1} c over the q active positions (position j in lane j), fp64
 // arithmetic with the fp32 R (column-major, zero diagonal) and its diagonal
@@ -168,15 +163,32 @@ __device__ __forceinline__ double minv(double c, int q, int l, const float *R, d
   return l < q ? zl : 0.0;
 }
 
-// sum_k w_k A[iam_k][l] over the active positions (lanes l < n), fp64
+// sum_k w_k A[iam_k][l] over the active positions (lanes l < n), fp64.
+// Each position's row is one coalesced load across the lanes; the loads go
+// out eight at a time before their FMAs (a load-use per position would
+// expose one L2 / Infinity-Cache round trip per active constraint).
 __device__ __forceinline__ double at_w(const double *__restrict__ Aq, int n, int q, int iam, double w, int l) {
-  double s = 0.0;
-  for (int kk = 0; kk < q; ++kk) {
-    const int row = __builtin_amdgcn_readlane(iam, kk);
-    const double u = readlane_d(w, kk);
-    s = __builtin_fma(u, (l < n) ? Aq[row * n + (l < n ? l : 0)] : 0.0, s);
+  // a fresh base pointer per call: the loads are loop-invariant across the
+  // refinement steps, and hoisted out of the loop they would pin up to 64 VGPRs
+  asm volatile("" : "+s"(Aq));
+  double s0 = 0.0, s1 = 0.0;
+  const int lc = l < n ? l : 0;
+  for (int k0 = 0; k0 < q; k0 += 8) {  // wave-uniform
+    double a[8], u[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int kk = k0 + t < q ? k0 + t : q - 1;  // clamped: a duplicate row with u = 0
+      const int row = __builtin_amdgcn_readlane(iam, kk);
+      u[t] = k0 + t < q ? readlane_d(w, kk) : 0.0;
+      a[t] = Aq[row * n + lc];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (t % 2 == 0) s0 = __builtin_fma(u[t], a[t], s0);
+      else s1 = __builtin_fma(u[t], a[t], s1);
+    }
   }
-  return s;
+  return l < n ? s0 + s1 : 0.0;
 }
 
 template <int OCC>
@@ -476,59 +488,209 @@ __global__ __launch_bounds__(64, OCC) void gi_mixed_kernel(
   // ------------------------------------------- fp64 refinement of the KKT system
   bool redo = status != QPB_OK;
   double xl = 0.0, lam = (l < q) ? (double)um : 0.0;
-  if (!redo) {
-    const int ll = l & (NP - 1);
+  if (!redo && QPB_MX_STAGE >= 1) {
+    const int h = l >> 5, c = l & (NP - 1);
+    // explicit fp32 U = R^{-1} (upper triangular, M^{-1} = U U^T): lane j
+    // solves R u = e_j right-looking over the columns of R (contiguous in
+    // LDS); the diagonal of R goes through LDS first
     wave_lds_sync();
-    const double invd = ll < n ? 1.0 / (double)Lp[lrow(ll) + ll] : 0.0;
-    const double ird = (l < q) ? 1.0 / (double)rdg : 0.0;
-    const double *hrow = Hq + (l < n ? l : 0) * n;
+    if (l < NP) xch[l] = (l < q) ? rdg : 1.f;
+    wave_lds_sync();
+    {
+      float U[NP];
+#pragma unroll
+      for (int k = 0; k < NP; ++k) U[k] = 0.f;
+      unroll<NP>([&](auto II) {
+        constexpr int i = NP - 1 - II;
+        if (i >= q) return;  // wave-uniform
+        wave_lds_sync();
+        int cc = c;
+        asm volatile("" : "+v"(cc));
+        const float ui = ((cc == i) ? 1.f : U[i]) * __builtin_amdgcn_rcpf(xch[i]);
+        U[i] = ui;
+        unroll<i>([&](auto K) {
+          constexpr int k = K;
+          U[k] = __builtin_fmaf(-R[i * NP + k], ui, U[k]);
+        });
+        unroll<i + 1>([&](auto K) {
+          constexpr int k = K;
+          pinf(U[k]);
+        });
+      });
+      wave_lds_sync();  // every lane has read R: U overwrites it, column j by lane j
+      if (l < q) {
+#pragma unroll
+        for (int k = 0; k < NP; k += 4)
+          *reinterpret_cast<float4 *>(&R[l * NP + k]) = make_float4(U[k], U[k + 1], U[k + 2], U[k + 3]);
+      }
+      wave_lds_sync();
+    }
+    // explicit fp32 H^{-1} = L^{-T} L^{-1}: lane l solves for column c (= row
+    // c), L's entries read from LDS as broadcasts (rows >= n of L are zero)
+    wave_lds_sync();
+    float Hi[NP];
+    unroll<NP>([&](auto K) {  // L y = e_c
+      constexpr int k = K;
+      // one row of L at a time: the ordering point keeps the step's LDS reads
+      // from being hoisted (all 528 would be live at once), the opaque copy
+      // of c keeps the lane test from becoming 32 hoisted SGPR masks
+      wave_lds_sync();
+      int cc = c;
+      asm volatile("" : "+v"(cc));
+      float acc = (cc == k) ? 1.f : 0.f;
+      unroll<k>([&](auto I) {
+        constexpr int i = I;
+        acc = __builtin_fmaf(-Lp[lrow(k) + i], Hi[i], acc);
+      });
+      const float dk = Lp[lrow(k) + k];
+      Hi[k] = k < n ? acc * __builtin_amdgcn_rcpf(dk) : 0.f;
+      asm volatile("" : "+v"(Hi[k]));  // materialised here: IR passes would sink the step's FMAs
+    });
+    // the backward pass reads the same entries again: this ordering point
+    // keeps the compiler from holding all 528 across the two passes
+    wave_lds_sync();
+    unroll<NP>([&](auto KK) {  // L^T z = y
+      constexpr int k = NP - 1 - KK;
+      wave_lds_sync();
+      float acc = Hi[k];
+      unroll<NP - 1 - k>([&](auto I) {
+        constexpr int i = k + 1 + I;
+        acc = __builtin_fmaf(-Lp[lrow(i) + k], Hi[i], acc);
+      });
+      const float dk = Lp[lrow(k) + k];
+      Hi[k] = k < n ? acc * __builtin_amdgcn_rcpf(dk) : 0.f;
+      asm volatile("" : "+v"(Hi[k]));
+    });
+    // (H^{-1} r)_c, r broadcast through LDS (lanes < 32 hold components)
+    auto hinv_apply = [&](double r) -> double {
+      wave_lds_sync();
+      if (l < NP) xd[l] = (l < n) ? r : 0.0;
+      wave_lds_sync();
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < NP; j += 2) {
+        if (j % 8 == 0) wave_lds_sync();  // eight reads in flight at a time (register budget)
+        const double2 v = *reinterpret_cast<const double2 *>(&xd[j]);
+        // opaque copies: the fp64 conversions of H^{-1} stay inside each call
+        // (hoisted out of the refinement loop they would hold 64 VGPRs)
+        float h0 = Hi[j], h1 = Hi[j + 1];
+        asm volatile("" : "+v"(h0), "+v"(h1));
+        a0 = __builtin_fma((double)h0, v.x, a0);
+        a1 = __builtin_fma((double)h1, v.y, a1);
+      }
+      return (c < n) ? a0 + a1 : 0.0;
+    };
+    // (H x)_c in fp64.  H is read two rows per load instruction (coalesced):
+    // lane l gets H[2i+h][c] = H[c][2i+h] (symmetric), half of row c, so the
+    // dot is a half-row partial plus the other half's (lane ^ 32).  Re-read
+    // per call (L2 / Infinity Cache): held across the refinement it would
+    // pin 32 VGPRs.
+    auto h_mul = [&](double x) -> double {
+      wave_lds_sync();
+      if (l < NP) xd[l] = (l < n) ? x : 0.0;
+      wave_lds_sync();
+      const double *Hp = Hq;
+      asm volatile("" : "+s"(Hp));
+      double a = 0.0;
+#pragma unroll
+      for (int i0 = 0; i0 < NP / 2; i0 += 8) {
+        double hv[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int r = 2 * (i0 + t) + h;
+          const bool ok = r < n && c < n;
+          const double v = Hp[ok ? r * n + c : 0];
+          hv[t] = ok ? v : 0.0;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) a = __builtin_fma(hv[t], xd[2 * (i0 + t) + h], a);
+      }
+      const double o = __shfl_xor(a, 32);
+      return (c < n) ? a + o : 0.0;
+    };
+    // (U U^T c) over the positions, fp64 arithmetic, c broadcast through LDS
+    auto minv2 = [&](double cv) -> double {
+      wave_lds_sync();
+      if (l < NP) xd[l] = (l < q) ? cv : 0.0;
+      wave_lds_sync();
+      double w = 0.0;  // w_j = sum_k U[k][j] c_k, lane j reads its column
+#pragma unroll
+      for (int k = 0; k < NP; k += 2) {
+        if (k % 8 == 0) wave_lds_sync();
+        const double2 v = *reinterpret_cast<const double2 *>(&xd[k]);
+        w = __builtin_fma((double)R[c * NP + k], v.x, w);
+        w = __builtin_fma((double)R[c * NP + k + 1], v.y, w);
+      }
+      wave_lds_sync();
+      if (l < NP) xd[l] = (l < q) ? w : 0.0;
+      wave_lds_sync();
+      double z = 0.0;  // z_i = sum_j U[i][j] w_j, lane i reads row i (strided)
+#pragma unroll
+      for (int j = 0; j < NP; j += 2) {
+        if (j % 8 == 0) wave_lds_sync();
+        const double2 v = *reinterpret_cast<const double2 *>(&xd[j]);
+        z = __builtin_fma((double)R[j * NP + c], v.x, z);
+        z = __builtin_fma((double)R[(j + 1) * NP + c], v.y, z);
+      }
+      return (l < q) ? z : 0.0;
+    };
     const double *arow = Aq + (l < q && iam >= 0 ? iam : 0) * n;
     const double bw = (l < q && iam >= 0) ? bq[iam] : 0.0;
     // x = -H^{-1} (f + A_W^T lam)
-    xl = -hinv(fv + at_w(Aq, n, q, iam, lam, l), n, l, Lp, invd);
-    double corr = 0.0;
-    for (int step = 0; step < kRefine; ++step) {
+    xl = -hinv_apply(fv + at_w(Aq, n, q, iam, lam, l));
+    const double x_init = xl;
+    // Refinement.  The error after a step is ~ kappa * (that step's
+    // correction), kappa the observed contraction (corr_s / corr_{s-1});
+    // stop once that estimate is below 1e-12
+    double corr = 1.0, corr_prev = 1.0;
+    bool converged = false;
+    for (int step = 0; step < (QPB_MX_STAGE >= 2 ? kRefine : 0) && !converged; ++step) {
+      // r1 = -f - H x - A_W^T lam; one A_W product per step: c = A_W (x + v) - b_W
+      const double hx = h_mul(xl);
+      const double r1 = (l < n) ? -(fv + hx + at_w(Aq, n, q, iam, lam, l)) : 0.0;
+      const double v = hinv_apply(r1);
+      wave_lds_sync();
+      if (l < NP) xd[l] = (l < n) ? xl + v : 0.0;
+      wave_lds_sync();
+      const double cc = (l < q) ? row_dot(arow, n, xd) - bw : 0.0;
+      const double dlam = minv2(cc);
+      const double dx = v - hinv_apply(at_w(Aq, n, q, iam, dlam, l));
+      xl += dx;
+      lam += dlam;
+      corr_prev = corr;
+      corr = wave_maxd(l < n ? __builtin_fabs(dx) : 0.0) / (1.0 + wave_maxd(l < n ? __builtin_fabs(xl) : 0.0));
+      converged = corr <= 1e-13 || (step > 0 && corr * (corr / corr_prev) <= 1e-12);
+    }
+    // ---- fp64 verification: lam >= 0, refinement converged, and every
+    // inactive row feasible.  A row whose fp32 normalised slack is beyond the
+    // fp32 solution's error (tau) is feasible in fp64 too; the others are
+    // checked in fp64 (their A rows re-read).
+    if (QPB_MX_STAGE >= 3) {
       wave_lds_sync();
       if (l < NP) xd[l] = (l < n) ? xl : 0.0;
       wave_lds_sync();
-      // r1 = -f - H x - A_W^T lam (components l < n); r2 = b_W - A_W x (positions l < q)
-      const double hx = (l < n) ? row_dot(hrow, n, xd) : 0.0;
-      const double r1 = (l < n) ? -(fv + hx + at_w(Aq, n, q, iam, lam, l)) : 0.0;
-      const double r2 = (l < q) ? bw - row_dot(arow, n, xd) : 0.0;
-      const double v = hinv(r1, n, l, Lp, invd);
-      wave_lds_sync();
-      if (l < NP) xd[l] = v;
-      wave_lds_sync();
-      const double c = (l < q) ? row_dot(arow, n, xd) - r2 : 0.0;
-      const double dlam = minv(c, q, l, R, ird);
-      const double dx = v - hinv(at_w(Aq, n, q, iam, dlam, l), n, l, Lp, invd);
-      xl += dx;
-      lam += dlam;
       const double xa = wave_maxd(l < n ? __builtin_fabs(xl) : 0.0);
-      corr = wave_maxd(l < n ? __builtin_fabs(dx) : 0.0) / (1.0 + xa);
-    }
-    // ---- fp64 verification: feasibility of every row, lam >= 0, converged
-    wave_lds_sync();
-    if (l < NP) xd[l] = (l < n) ? xl : 0.0;
-    wave_lds_sync();
-    bool bad = false;
-    if (rowok) {
-      const double *ar = Aq + l * n;
-      double an = 0.0;
+      const double dxi = wave_maxd(l < n ? __builtin_fabs(xl - x_init) : 0.0);
+      const double tau = 1e-3 * (1.0 + xa) + 64.0 * dxi;
+      bool bad = false;
+      if (rowok && !act && nrm2 > 0.f && (double)(s * invn) < tau) {
+        const double *ar = Aq + l * n;
+        double an = 0.0;
 #pragma unroll
-      for (int j = 0; j < NP; ++j)
-        if (j < n) an = __builtin_fma(ar[j], ar[j], an);
-      const double sl = bv - row_dot(ar, n, xd);
-      an = __builtin_sqrt(an);
-      bad = an > 0.0 && !act && sl < -feas_tol * (an + __builtin_fabs(bv));
+        for (int j = 0; j < NP; ++j)
+          if (j < n) an = __builtin_fma(ar[j], ar[j], an);
+        const double sl = bv - row_dot(ar, n, xd);
+        bad = sl < -feas_tol * (__builtin_sqrt(an) + __builtin_fabs(bv));
+      }
+      const double lmax = wave_maxd(l < q ? __builtin_fabs(lam) : 0.0);
+      if (l < q && lam < 0.0) {
+        if (lam < -1e-9 * (1.0 + lmax)) bad = true;
+        lam = 0.0;
+      }
+      bad = bad || !(__builtin_fabs(xl) < kInf) || !converged;
+      redo = wave_any(bad);
     }
-    const double lmax = wave_maxd(l < q ? __builtin_fabs(lam) : 0.0);
-    if (l < q && lam < 0.0) {
-      if (lam < -1e-9 * (1.0 + lmax)) bad = true;
-      lam = 0.0;
-    }
-    bad = bad || !(__builtin_fabs(xl) < kInf) || !(corr <= 1e-11);
-    redo = wave_any(bad);
   }
 
   // ------------------------------------------------------------- outputs
@@ -565,7 +727,7 @@ extern "C" hipError_t qpb_launch_gi_mixed(const qpb_desc *d, const double *H, co
                                           int32_t *status, int32_t *iters, hipStream_t stream) {
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
-  hipLaunchKernelGGL(qpb::mx::gi_mixed_kernel<4>, dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b, x, lam,
+  hipLaunchKernelGGL(qpb::mx::gi_mixed_kernel<QPB_MX_OCC>, dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b, x, lam,
                      active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || (d->flags & QPB_FLAG_DIAG_NO_REDO)) return e;
