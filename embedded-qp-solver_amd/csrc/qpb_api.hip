@@ -34,6 +34,8 @@ extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, con
                                      const double *x0, double *x, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
                                          const double *x, double *out, hipStream_t stream);
+extern "C" hipError_t qpb_launch_ref_invert(int n, long long batch, const double *P, double *Pinv,
+                                            hipStream_t stream);
 
 extern "C" hipError_t qpb_launch_ref_generate(int n, long long batch, unsigned long long first, unsigned seed,
                                               const double *range, double *P, double *q, double *x0,
@@ -262,6 +264,22 @@ extern "C" int qpb_ref_solve_host(const qpb_ref_desc *d, const double *P, const 
   HIPCHK(hipDeviceSynchronize(), "qpb_ref_solve_host kernel");
   HIPCHK(down(x, dx, B * n * 8), "x D2H");
   HIPCHK(down(iters, di, B * 4), "iters D2H");
+  return 0;
+}
+
+extern "C" int qpb_matrix_invert(int32_t n, int64_t batch, const double *P, double *Pinv, void *stream) {
+  if (n < 1 || batch < 0) return fail(QPB_ERR_INVALID_ARG, "bad qpb_matrix_invert arguments");
+  if (n > 64) return fail(QPB_ERR_UNSUPPORTED, "qpb_matrix_invert: n=%d > 64", n);
+  if (batch == 0) return 0;
+  if (!P || !Pinv) return fail(QPB_ERR_INVALID_ARG, "P and Pinv are required");
+  int rc = check_device();
+  if (rc) return rc;
+  const long long nn = (long long)n * n, step = 1LL << 25;  // one 64-thread workgroup per matrix
+  for (long long k0 = 0; k0 < batch; k0 += step) {
+    const long long c = batch - k0 < step ? batch - k0 : step;
+    hipError_t e = qpb_launch_ref_invert(n, c, P + k0 * nn, Pinv + k0 * nn, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "qpb_matrix_invert launch");
+  }
   return 0;
 }
 

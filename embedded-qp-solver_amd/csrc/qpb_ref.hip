@@ -327,7 +327,46 @@ __global__ void qf_eval_kernel(int n, long long batch, const double *__restrict_
   out[g] = a;
 }
 
+// Batched matrix_invert (matrix_ops.c:551-630) on its own: P -> P^{-1} per
+// QP, the same LU + per-column solves the Newton / ADMM replicas run.
+__global__ __launch_bounds__(REF_THREADS) void ref_invert_kernel(int n, long long batch,
+                                                                 const double *__restrict__ Pg,
+                                                                 double *__restrict__ Vg) {
+  extern __shared__ double sm[];
+  const long long g = blockIdx.x;
+  if (g >= batch) return;
+  const int tid = threadIdx.x;
+  const int nn2 = n * n;
+  RefShared S;
+  S.P = nullptr;
+  S.M = sm;
+  S.W = S.M + nn2;
+  S.V = S.W + nn2;
+  S.scal = S.V + nn2;
+  S.perm = reinterpret_cast<int *>(S.scal + 8);
+  const double *Pq = Pg + g * (long long)nn2;
+  for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = Pq[e];
+  __syncthreads();
+  ref_invert(S, n);
+  double *Vq = Vg + g * (long long)nn2;
+  for (int e = tid; e < nn2; e += blockDim.x) Vq[e] = S.V[e];
+}
+
 }  // namespace qpb
+
+extern "C" hipError_t qpb_launch_ref_invert(int n, long long batch, const double *P, double *Pinv,
+                                            hipStream_t stream) {
+  if (n > qpb::REF_MAXN) return hipErrorInvalidValue;
+  const size_t lds = sizeof(double) * (3 * (size_t)n * n + 8) + sizeof(int) * (qpb::REF_MAXN + 2);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&qpb::ref_invert_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(qpb::ref_invert_kernel, dim3((unsigned)batch), dim3(qpb::REF_THREADS), lds, stream, n, batch, P,
+                     Pinv);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
                                          const double *x, double *out, hipStream_t stream) {

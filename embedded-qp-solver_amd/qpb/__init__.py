@@ -68,6 +68,8 @@ _lib.qpb_ref_solve_host.argtypes = [ctypes.POINTER(RefDesc)] + [_vp] * 5
 _lib.qpb_ref_solve_host.restype = ctypes.c_int
 _lib.qpb_qf_eval.argtypes = [ctypes.c_int32, ctypes.c_int64, _vp, _vp, ctypes.c_double, _vp, _vp, _vp]
 _lib.qpb_qf_eval.restype = ctypes.c_int
+_lib.qpb_matrix_invert.argtypes = [ctypes.c_int32, ctypes.c_int64, _vp, _vp, _vp]
+_lib.qpb_matrix_invert.restype = ctypes.c_int
 _lib.qpb_last_error.restype = ctypes.c_char_p
 _lib.qpb_version.restype = ctypes.c_char_p
 _lib.qpb_device_count.restype = ctypes.c_int
@@ -198,6 +200,15 @@ def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), s
                             _ptr(x), _ptr(it), _stream_ptr(stream))
     _check(rc, "qpb_ref_solve")
     return x, it
+
+
+def matrix_invert(P, stream=None):
+    """Batched reference matrix_invert (matrix_ops.c:551-630) of (B, n, n) CUDA tensors."""
+    import torch
+    B, n, _ = P.shape
+    out = torch.empty_like(P)
+    _check(_lib.qpb_matrix_invert(n, B, _ptr(P), _ptr(out), _stream_ptr(stream)), "qpb_matrix_invert")
+    return out
 
 
 def qf_eval(P, q, r: float, x, stream=None):

@@ -148,6 +148,15 @@ int qpb_ref_solve_host(const qpb_ref_desc *desc, const double *P,
 		       const double *q, const double *x0, double *x,
 		       int32_t *iters);
 
+/* Batched matrix_invert (matrix_ops.c:551-630): Pinv = P^{-1} per matrix,
+ * n <= 64, device pointers, n*n doubles each.  The reference's partial-pivot
+ * LU (first strict maximum, physical row swaps, :434-536) and per-column
+ * forward / back solves, unfused, in its order: bitwise equal to the
+ * reference's result.  A singular pivot stops the LU as in the reference
+ * (:511-515); the result is then garbage, as there. */
+int qpb_matrix_invert(int32_t n, int64_t batch, const double *P, double *Pinv,
+		      void *stream);
+
 /* f(x) = 1/2 x^T P x + q^T x + r per QP (qp.c:9-27), batched, device. */
 int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
 		double r, const double *x, double *out, void *stream);

@@ -65,3 +65,29 @@ def test_bad_files_are_rejected(tmp_path):
         qpb.wire_read(str(tmp_path / "badn.bin"))
     with pytest.raises(qpb.QPBError):
         qpb.wire_read(str(tmp_path / "missing.bin"))
+
+
+REF_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref")
+
+
+@pytest.mark.parametrize("n,seed", [(4, 7), (4, 20261015), (16, 1), (16, 99)])
+def test_bytes_of_the_reference_writer(tmp_path, n, seed):
+    """Pinned to the reference itself: oracle/_ref/wire_ref_n<N> runs the
+    unmodified test_reference() (test/test.c:108-130) on a QP from the
+    reference generator and keeps the file it writes (wire_driver.c).  Our
+    writer must produce the same bytes and our reader must return its P, q."""
+    import subprocess
+    exe = os.path.join(REF_DIR, f"wire_ref_n{n}")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref not built (make -C oracle ref, where /root/reference exists)")
+    subprocess.run([exe, str(seed)], cwd=tmp_path, check=True, timeout=60)
+    ref_bytes = (tmp_path / "wire_ref.bin").read_bytes()
+    pq = np.frombuffer((tmp_path / "pq.bin").read_bytes(), dtype=np.float64)
+    P, q = pq[: n * n].reshape(1, n, n), pq[n * n:].reshape(1, n)
+    ours = tmp_path / "ours.bin"
+    qpb.wire_write(str(ours), P, q)
+    assert ours.read_bytes() == ref_bytes
+    H2, f2, A2, b2 = qpb.wire_read(str(tmp_path / "wire_ref.bin"))
+    assert np.array_equal(H2[0], P[0]) and np.array_equal(f2[0], q[0]) and A2.shape == (1, 0, n)
+    nn, P3, q3 = oracle.read_wire(str(tmp_path / "wire_ref.bin"))  # qp_ref.py:8-30 restated
+    assert nn == n and np.array_equal(P3, P[0]) and np.array_equal(q3, q[0])
