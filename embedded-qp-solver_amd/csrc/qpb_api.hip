@@ -30,6 +30,10 @@ extern "C" hipError_t qpb_launch_gi_mixed(const qpb_desc *d, const double *H, co
 extern "C" hipError_t qpb_launch_gi_block(const qpb_desc *d, const double *H, const double *f, const double *A,
                                           const double *b, double *x, double *lam, uint32_t *active,
                                           int32_t *status, int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                         const double *b, double *x, double *lam, uint32_t *active,
+                                         int32_t *status, int32_t *iters, unsigned long long *sections,
+                                         hipStream_t stream);
 extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q,
                                      const double *x0, double *x, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
@@ -127,8 +131,10 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
       e = qpb_launch_gi_mixed(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
     else if (d->n <= 32 && d->m <= 64)
       e = qpb_launch_gi_wave(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
-    else
+    else if (d->flags & QPB_FLAG_DIAG_BLOCK)
       e = qpb_launch_gi_block(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
+    else
+      e = qpb_launch_gi_gram(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, nullptr, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
   }
   return 0;
@@ -141,14 +147,18 @@ extern "C" int qpb_solve_sections(const qpb_desc *d, const double *H, const doub
   if (rc) return rc;
   if (d->batch == 0) return 0;
   const bool n16 = d->n == 16 && d->m > 16 && d->m <= 32, wave = d->n > 16 && d->n <= 32 && d->m <= 64;
-  if (!(n16 || wave) || !sections)
-    return fail(QPB_ERR_UNSUPPORTED, "sections: n=16 with 16<m<=32, or 16<n<=32 with m<=64");
+  const bool gram = !(d->n <= 32 && d->m <= 64) && d->batch <= chunk_qps(d->n, d->m);
+  if (!(n16 || wave || gram) || !sections)
+    return fail(QPB_ERR_UNSUPPORTED, "sections: n=16 with 16<m<=32, 16<n<=32 with m<=64, or the n<=128 class");
   rc = check_device();
   if (rc) return rc;
-  hipError_t e = n16 ? qpb_launch_gi_sections(d, H, f, A, b, x, lam, active, status, iters, sections,
-                                              (hipStream_t)stream)
-                     : qpb_launch_gi_wave_sections(d, H, f, A, b, x, lam, active, status, iters, sections,
-                                                   (hipStream_t)stream);
+  hipError_t e;
+  if (n16)
+    e = qpb_launch_gi_sections(d, H, f, A, b, x, lam, active, status, iters, sections, (hipStream_t)stream);
+  else if (wave)
+    e = qpb_launch_gi_wave_sections(d, H, f, A, b, x, lam, active, status, iters, sections, (hipStream_t)stream);
+  else
+    e = qpb_launch_gi_gram(d, H, f, A, b, x, lam, active, status, iters, sections, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "qpb_solve_sections launch");
   return 0;
 }

@@ -1,0 +1,762 @@
+// qpb_gi_gram.hip -- active-set QP kernel for 32 < n <= 128, m <= 256 (gfx950).
+//
+// BASELINE configs[3] (n = 128, m = 256).  The same dual active-set method as
+// qpb_gi.hip (Goldfarb & Idnani), restated on the Gram matrix of the
+// constraint rows so that the big operand never changes after the setup:
+//
+//   setup   H = L L^T (blocked, right-looking, 16 x 16 tiles: trailing updates
+//           and panel solves on the fp64 matrix cores, v_mfma_f64_16x16x4_f64),
+//           D = A L^{-T} (blocked forward substitution, every tile product and
+//           the diagonal-tile solves on the matrix cores), y = L^{-1} f,
+//           s = b + D y (the slack of the unconstrained minimiser,
+//           test/qp_ref.py:35's answer).
+//   iterate for the selected row p (most violated normalised slack):
+//           u = D[p,:], v = D u (= column p of G = D D^T), c = v[W],
+//           r = G_WW^{-1} c (explicit inverse, updated by bordering),
+//           w = u - D_W^T r, |w|^2 (= |d2|^2 of G-I), slack direction D w,
+//           partial step t1 (ratio test on the multipliers), full step
+//           t2 = -s_p / |w|^2, s += t D w.
+//           ADD p: G_WW^{-1} grows by the bordering formula, D_W gains row u.
+//           DROP k: G_WW^{-1} loses row / column k by the Schur-complement
+//           downdate, D_W loses row k.  D itself is never rotated: the
+//           factor updates are O(q^2), the per-iteration big work is two
+//           GEMVs with D (v = D u and D w).
+//   finish  x = -L^{-T} (y + D_W^T lam) (KKT stationarity), L recomputed.
+//
+// Replaces, batched, the reference's dense kernels on this path: matrix_mult
+// (matrix_ops.c:235-271) as the MFMA tile products and the GEMVs, the LU /
+// explicit inverse (:487-630) by the Cholesky and the triangular solves, the
+// vector ops (:158-411) fused into the iteration.
+//
+// One QP per 1024-thread workgroup (16 wavefronts, four per SIMD), one
+// workgroup per CU; the workgroups pull QP indices from an atomic queue, so
+// QPs with long iteration counts do not hold up a static partition.
+// Registers: wave w owns rows 16w..16w+15 of D as eight 16 x 16 tiles in the
+// matrix cores' C/D layout, which is also their B-operand layout: lane
+// (g = l >> 4, j = l & 15) holds D[16w + j][16k + g + 4r] (tile k, element r),
+// i.e. row j, the 32 columns congruent to g mod 4.  A row dot product is
+// 32 FMAs and two cross-group butterfly steps.
+// LDS (160 KiB): the packed lower triangle (L in setup and finish, G_WW^{-1}
+// in the loop), the diagonal-tile inverses (setup) / the active rows D_W
+// (loop; rows past QL live in a per-workgroup global scratch), vectors.
+#include "qpb_common.h"
+#include "qpb.h"
+
+namespace qpb {
+namespace gram {
+
+constexpr int NB = 128;                // max (padded) n
+constexpr int MB = 256;                // max m: 16 rows per wavefront
+constexpr int NT = 512;   // 8 wavefronts, two per SIMD (256 VGPRs each)
+constexpr int NWV = NT / 64;
+constexpr int RT = MB / 16 / NWV;  // 16-row tiles of D per wavefront (2)
+constexpr int LP = NB * (NB + 1) / 2;  // packed triangle, 8256 doubles
+constexpr int LDS_D = 20480;           // 160 KiB
+constexpr int NBUF = 1024;
+constexpr int OFF_TRI = 0;
+constexpr int OFF_ROWS = LP;  // diagonal-tile inverses (setup) / D_W rows (loop)
+constexpr int OFF_BUF = LDS_D - NBUF;
+constexpr int QL = (OFF_BUF - OFF_ROWS) / NB;  // D_W rows in LDS (87)
+constexpr int B_U = OFF_BUF;                   // u = D[p,:] (permuted column order)
+constexpr int B_W = B_U + NB;                  // w (permuted)
+constexpr int B_V = B_W + NB;                  // v = D u (by row); lambda scatter at the end
+constexpr int B_R = B_V + MB;                  // r by active position
+constexpr int B_LAM = B_R + NB;                // multipliers by active position
+constexpr int B_Y = B_LAM + NB;                // y (permuted), then y + D_W^T lam
+constexpr int B_RED = B_Y + NB;                // selection keys, partial reductions, scalars
+constexpr int B_INT = B_RED + 32;              // ints: flags, queue slot, mask halves (64)
+constexpr int B_IAM = B_INT + 32;              // ints: constraint index by position (128)
+static_assert(B_IAM + 64 == LDS_D, "LDS layout");
+static_assert(OFF_ROWS + 8 * 256 <= OFF_BUF, "diagonal-tile inverses fit the row area");
+// B_RED slots
+constexpr int R_KEY = 0;    // per-wave selection keys (NWV)
+constexpr int R_T1 = 16;    // 2 per-wave (ratio min, argmin position)
+constexpr int R_ND2 = 20;   // 2 per-wave partial |w|^2
+constexpr int R_SP = 22;    // s_p
+constexpr double kDepTol = 1e-24;
+constexpr long long SCRATCH = LP + (long long)(NB - QL) * NB;  // doubles per workgroup
+
+using d4 = __attribute__((__vector_size__(4 * sizeof(double)))) double;
+
+__device__ __forceinline__ int tri(int i, int j) { return ((i * (i + 1)) >> 1) + j; }
+// column c -> its place in the permuted vector layout (lane group c & 3 reads
+// a contiguous 32-double block in the order of its registers)
+__device__ __forceinline__ int perm(int c) { return ((c & 3) << 5) + ((c >> 4) << 2) + ((c >> 2) & 3); }
+__device__ __forceinline__ double mfma(double a, double b, d4 &c) {
+  c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  return 0.0;
+}
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double pack_key256(double v, int idx) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  return __builtin_bit_cast(double, (b & ~255ull) | (unsigned long long)idx);
+}
+__device__ __forceinline__ int key_index256(double k) { return (int)(__builtin_bit_cast(unsigned long long, k) & 255ull); }
+// min over the 64 lanes of a wave (exact), on every lane
+__device__ __forceinline__ double wave_min(double v) {
+  v = row_min(v);
+  return __builtin_fmin(__builtin_fmin(readlane_d(v, 0), readlane_d(v, 16)),
+                        __builtin_fmin(readlane_d(v, 32), readlane_d(v, 48)));
+}
+__device__ __forceinline__ double wave_sum(double v) {
+  v = row_sum(v);
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+// sum over the four lane groups (lanes j, j+16, j+32, j+48): the same value,
+// bitwise, on all four.  gfx950's v_permlane32_swap / v_permlane16_swap with
+// one register as both operands hand every lane the pair {value of the lower
+// partner, value of the upper partner} (lanes l, l ^ 32, resp. l, l ^ 16;
+// tools/probe/permlane_probe.hip), so both partners add the same two numbers
+// in the same order.
+__device__ __forceinline__ double pair32(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  const double x = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+  const double y = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+  return x + y;
+}
+__device__ __forceinline__ double pair16(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  const double x = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+  const double y = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+  return x + y;
+}
+__device__ __forceinline__ double group_sum(double v) { return pair16(pair32(v)); }
+// this lane's rows of D (one per tile) against a permuted vector in LDS
+__device__ __forceinline__ void row_dot(const double (&E)[RT][8][4], const double *vp, double (&out)[RT]) {
+  double a[RT][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[t][r] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double2 x = *reinterpret_cast<const double2 *>(&vp[4 * k]);
+    const double2 y = *reinterpret_cast<const double2 *>(&vp[4 * k + 2]);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      a[t][0] = __builtin_fma(E[t][k][0], x.x, a[t][0]);
+      a[t][1] = __builtin_fma(E[t][k][1], x.y, a[t][1]);
+      a[t][2] = __builtin_fma(E[t][k][2], y.x, a[t][2]);
+      a[t][3] = __builtin_fma(E[t][k][3], y.y, a[t][3]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < RT; ++t) out[t] = group_sum((a[t][0] + a[t][1]) + (a[t][2] + a[t][3]));
+}
+// symmetric packed access
+__device__ __forceinline__ double sym(const double *P, int i, int j) { return i >= j ? P[tri(i, j)] : P[tri(j, i)]; }
+
+// ---------------------------------------------------------------- Cholesky
+// H (n x n, padded to 16 T with the identity) from global memory into the
+// packed lower triangle, factorised in place: blocked right-looking over
+// 16 x 16 tiles.  The diagonal tile is factorised by wavefront 0 (lane i owns
+// row i, pivot rows by DPP broadcast as in qpb_gi.hip) and inverted (lane j
+// solves column j); the panel below it is multiplied by that inverse and the
+// trailing tiles updated on the matrix cores.  Returns false if a pivot <= 0.
+__device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__ Hq, int n, int T) {
+  double *Lp = lds + OFF_TRI;
+  double *LI = lds + OFF_ROWS;
+  int *flags = reinterpret_cast<int *>(lds + B_INT);
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int nb = 16 * T;
+  for (int r = wv; r < nb; r += NWV)  // row r, lanes along the columns (coalesced)
+    for (int c = l; c <= r; c += 64) Lp[tri(r, c)] = (r < n) ? Hq[r * n + c] : (r == c ? 1.0 : 0.0);
+  if (tid == 0) flags[0] = 0;
+  __syncthreads();
+  for (int K = 0; K < T; ++K) {
+    if (wv == 0) {
+      int i = l & 15;
+      asm volatile("" : "+v"(i));  // opaque per step: nothing lane-dependent is hoisted and kept live
+      const int r0 = 16 * K;
+      // lane i: row i of the tile (a, the full symmetric row) and row i of
+      // the identity (e): the sweep turns e into row i of L^{-T}, i.e.
+      // column i of the tile inverse, alongside the factorisation
+      double a[16], e[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        a[j] = j <= i ? Lp[tri(r0 + i, r0 + j)] : Lp[tri(r0 + j, r0 + i)];
+        e[j] = j == i ? 1.0 : 0.0;
+      }
+      bool ok = true;
+      unroll<16>([&](auto Kc) {
+        constexpr int k = Kc;
+        // pivot row k of the Schur complement = column k (symmetry): lane k's
+        // entries, broadcast by DPP
+        const double akk = bc<k>(a[k]);
+        ok = ok && (akk > 0.0);
+        const double ik = rsq(akk);
+        const double ik2 = ik * ik;
+        const double c = a[k] * ik2;
+        const double ne2 = -(e[k] * ik2);
+        e[k] *= ik;
+        unroll<15 - k>([&](auto J) {
+          constexpr int j = k + 1 + J;
+          const double pj = bc<k>(a[j]);
+          e[j] = __builtin_fma(ne2, pj, e[j]);
+          a[j] = __builtin_fma(-c, pj, a[j]);
+          // materialised inside the step: IR passes would otherwise sink the
+          // updates and keep every step's broadcasts alive (qpb_gi.hip)
+          pin(e[j]);
+          pin(a[j]);
+        });
+        a[k] *= ik;
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      if (l < 16) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (j <= i) Lp[tri(r0 + i, r0 + j)] = a[j];
+          LI[K * 256 + j * 16 + i] = e[j];
+        }
+      }
+      if (l == 0 && !ok) flags[0] = 1;
+    }
+    __syncthreads();
+    // panel: L[I, K] = H~[I, K] Linv_K^T, one tile per wavefront
+    const int li = l & 15, lk = l >> 4;
+    if (wv < T - K - 1) {
+      const int I = K + 1 + wv;
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        mfma(Lp[tri(16 * I + li, 16 * K + 4 * s + lk)], LI[K * 256 + li * 16 + 4 * s + lk], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Lp[tri(16 * I + lk + 4 * r, 16 * K + li)] = acc[r];
+    }
+    __syncthreads();
+    // trailing tiles (I, J), K < J <= I < T, round robin over the wavefronts
+    const int nr = T - K - 1, ntile = nr * (nr + 1) / 2;
+    for (int t = wv; t < ntile; t += NWV) {
+      int I = (int)((__builtin_sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      if (tri(I + 1, 0) <= t) ++I;
+      if (tri(I, 0) > t) --I;
+      int J = t - tri(I, 0);
+      I += K + 1;
+      J += K + 1;
+      d4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I + lk + 4 * r, col = 16 * J + li;
+        acc[r] = row >= col ? Lp[tri(row, col)] : 0.0;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        mfma(-Lp[tri(16 * I + li, 16 * K + 4 * s + lk)], Lp[tri(16 * J + li, 16 * K + 4 * s + lk)], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I + lk + 4 * r, col = 16 * J + li;
+        if (row >= col) Lp[tri(row, col)] = acc[r];
+      }
+    }
+    __syncthreads();
+  }
+  return flags[0] == 0;
+}
+
+// Lane-parallel triangular solves with the packed L on one wavefront: lane l
+// owns entries l and l + 64 (a0, a1: right-hand side in, solution out).
+// Step i broadcasts the finished entry i (v_readlane with a constant lane) and
+// every later entry takes its update; the steps are unrolled over the whole
+// padded size (entries past nb have zero rows), L prefetched 16 steps at a
+// time, so only the broadcast chain is serial.  A finished entry is never
+// touched again (its later coefficients are zero), so the solution is the
+// accumulator times 1 / L_ii at the end.
+__device__ __forceinline__ void solve_lower(const double *Lp, int nb, int l, double &a0, double &a1) {
+  const double id0 = l < nb ? rcp(Lp[tri(l, l)]) : 0.0;
+  const double id1 = l + 64 < nb ? rcp(Lp[tri(l + 64, l + 64)]) : 0.0;
+  unroll<8>([&](auto C) {
+    constexpr int i0 = 16 * C;
+    double L0[16], L1[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int i = i0 + jj;
+      L0[jj] = (i0 < 64 && l > i && l < nb) ? Lp[tri(l, i)] : 0.0;
+      L1[jj] = (l + 64 > i && l + 64 < nb) ? Lp[tri(l + 64, i)] : 0.0;
+    }
+    unroll<16>([&](auto J) {
+      constexpr int i = i0 + J;
+      if constexpr (i < 64) {
+        const double yi = readlane_d(a0 * id0, i);
+        a0 = __builtin_fma(-L0[J], yi, a0);
+        a1 = __builtin_fma(-L1[J], yi, a1);
+      } else {
+        const double yi = readlane_d(a1 * id1, i - 64);
+        a1 = __builtin_fma(-L1[J], yi, a1);
+      }
+    });
+  });
+  a0 *= id0;
+  a1 *= id1;
+}
+// L^T x = v (backward)
+__device__ __forceinline__ void solve_upper(const double *Lp, int nb, int l, double &a0, double &a1) {
+  const double id0 = l < nb ? rcp(Lp[tri(l, l)]) : 0.0;
+  const double id1 = l + 64 < nb ? rcp(Lp[tri(l + 64, l + 64)]) : 0.0;
+  unroll<8>([&](auto C) {
+    constexpr int i1 = 112 - 16 * C;
+    double L0[16], L1[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int i = i1 + jj;
+      L0[jj] = (l < i && i < nb) ? Lp[tri(i, l)] : 0.0;
+      L1[jj] = (i1 >= 64 && l + 64 < i && i < nb) ? Lp[tri(i, l + 64)] : 0.0;
+    }
+    unroll<16>([&](auto J) {
+      constexpr int i = i1 + 15 - J;
+      if constexpr (i >= 64) {
+        const double xi = readlane_d(a1 * id1, i - 64);
+        a0 = __builtin_fma(-L0[15 - J], xi, a0);
+        a1 = __builtin_fma(-L1[15 - J], xi, a1);
+      } else {
+        const double xi = readlane_d(a0 * id0, i);
+        a0 = __builtin_fma(-L0[15 - J], xi, a0);
+      }
+    });
+  });
+  a0 *= id0;
+  a1 *= id1;
+}
+
+// ------------------------------------------------------ D_W row storage
+struct Rows {
+  double *lds;  // rows 0..QL-1
+  double *gl;   // rows QL.. (per-workgroup global scratch)
+  __device__ __forceinline__ double *row(int j) const { return j < QL ? lds + j * NB : gl + (j - QL) * NB; }
+};
+
+// ------------------------------------------------------------------ kernel
+template <bool STAMP>
+__global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
+    const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
+    const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg, uint32_t *__restrict__ actg,
+    int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m, long long batch, int max_iter,
+    double feas_tol, int *__restrict__ queue, double *__restrict__ scratch, unsigned long long *__restrict__ dbg) {
+  __shared__ double lds[LDS_D];
+  // diagnostic build: s_memrealtime section stamps (0 Cholesky, 1 D, 2 y and
+  // s, 3 select + v, 4 r + ratio, 5 w, 6 step + update, 7 outputs, 8 L again,
+  // 9 x, 10 queue)
+  SectionClock<STAMP> clk;
+  double *Lp = lds + OFF_TRI;  // L, then G_WW^{-1} (packed lower)
+  double *LI = lds + OFF_ROWS;
+  double *ub = lds + B_U, *wb = lds + B_W, *vb = lds + B_V, *rb = lds + B_R, *lamb = lds + B_LAM, *yb = lds + B_Y;
+  double *red = lds + B_RED;
+  int *flags = reinterpret_cast<int *>(lds + B_INT);
+  int *iamb = reinterpret_cast<int *>(lds + B_IAM);
+  // per-workgroup scratch: L (packed), then the D_W rows past QL
+  double *Lgl = scratch + (long long)blockIdx.x * SCRATCH;
+  const Rows DW{lds + OFF_ROWS, Lgl + LP};
+  const int T = (n + 15) >> 4, nb = 16 * T;
+  for (;;) {
+    // lane ids re-derived opaquely per QP: lane-dependent values are not
+    // hoisted out of the QP loop (they would stay live across it)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int l = tid & 63, wv = tid >> 6;
+    const int li = l & 15, lk = l >> 4;  // lane: row li of each of the wave's tiles, column group lk
+    int row[RT];
+    bool rowok[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      row[t] = 16 * (RT * wv + t) + li;
+      rowok[t] = row[t] < m;
+    }
+    if (tid == 0) flags[1] = atomicAdd(queue, 1);
+    __syncthreads();
+    const long long g = flags[1];
+    if (g >= batch) break;
+    const double *Hq = Hg + g * (long long)n * n;
+    const double *Aq = Ag + g * (long long)m * n;
+
+    // ------------------------------------------------------------ setup
+    clk.tick(10);
+    const bool spd = cholesky(lds, Hq, n, T);
+#ifdef GRAM_ONLY_CHOL
+    if (tid == 0) statg[g] = spd;
+    continue;
+#endif
+    // L kept in the workgroup's scratch for the final solve (the triangle
+    // holds G_WW^{-1} during the loop); the loads back come after several
+    // barriers on the same CU
+    for (int e = tid; e < tri(nb, 0); e += NT) Lgl[e] = Lp[e];
+    clk.tick(0);
+    // y = L^{-1} f on wavefront 0, into yb (permuted), before D is live
+    if (wv == 0) {
+      double a0 = l < n ? fg[g * n + l] : 0.0, a1 = l + 64 < n ? fg[g * n + l + 64] : 0.0;
+      solve_lower(Lp, nb, l, a0, a1);
+      yb[perm(l)] = a0;
+      yb[perm(l + 64)] = a1;
+    }
+
+    // D = A L^{-T} on the matrix cores: tile k of D^T (16 columns of D x 16
+    // rows) = (A^T's tile - sum_{j<k} L[k, j] D^T[j]) times Linv_k; the two
+    // row tiles of the wave share every L operand
+    double E[RT][8][4];
+    double na2[RT] = {};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[t][k][r] = 0.0;
+      if (k < T) {
+        d4 C[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = 16 * k + lk + 4 * r;
+            C[t][r] = (rowok[t] && col < n) ? Aq[row[t] * n + col] : 0.0;
+            na2[t] = __builtin_fma(C[t][r], C[t][r], na2[t]);
+          }
+#pragma unroll
+        for (int j = 0; j < k; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const double a = -Lp[tri(16 * k + li, 16 * j + 4 * s + lk)];
+#pragma unroll
+            for (int t = 0; t < RT; ++t) mfma(a, E[t][j][s], C[t]);
+          }
+        d4 Z[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) Z[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double a = LI[k * 256 + li * 16 + 4 * s + lk];
+#pragma unroll
+          for (int t = 0; t < RT; ++t) mfma(a, C[t][s], Z[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) E[t][k][r] = Z[t][r];
+      }
+    }
+    clk.tick(1);
+    double bl[RT], invn[RT], thr[RT], s[RT];
+    bool zero_bad = false, act[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const double nn2 = group_sum(na2[t]);
+      bl[t] = rowok[t] ? bg[g * m + row[t]] : 0.0;
+      invn[t] = nn2 > 0.0 ? rsq(nn2) : 0.0;
+      thr[t] = (rowok[t] && nn2 > 0.0) ? -feas_tol * (1.0 + __builtin_fabs(bl[t]) * invn[t]) : -kInf;
+      zero_bad = zero_bad || (rowok[t] && nn2 == 0.0 && bl[t] < -feas_tol * (1.0 + __builtin_fabs(bl[t])));
+      act[t] = false;
+    }
+    if (tid == 0) flags[20] = 0;
+    __syncthreads();
+    if (zero_bad && lk == 0) flags[20] = 1;
+    {
+      double dy[RT];
+      row_dot(E, yb + 32 * lk, dy);  // s = b + D y
+#pragma unroll
+      for (int t = 0; t < RT; ++t) s[t] = bl[t] + dy[t];
+    }
+    __syncthreads();
+    int status = !spd ? QPB_NOT_SPD : (flags[20] ? QPB_INFEASIBLE : QPB_MAX_ITER);
+    bool done = status != QPB_MAX_ITER;
+    clk.tick(2);
+
+    // ------------------------------------------------------- active set
+    // The active constraints live in SLOTS (0 .. hi-1, occupancy mask occ):
+    // slot j holds a row index (iamb), its multiplier (lamb), its row of D
+    // (D_W) and row / column j of G_WW^{-1} (zero for free slots, so sums
+    // may run over every slot below hi).  A DROP frees a slot, an ADD takes
+    // the lowest free one: nothing is ever shifted.  Row i of the packed
+    // inverse belongs to threads 8 (i mod NT/8) + c, columns c, c + 8, ...
+    int q = 0, it = 0, p = 0, hi = 0;
+    unsigned long long occ0 = 0, occ1 = 0;  // slot occupancy (uniform)
+    bool selecting = true;
+    double up = 0.0;
+    auto publish_key = [&]() {
+      double key = kBig;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const double v = s[t] * invn[t];
+        key = (lk == 0 && !act[t] && v < thr[t]) ? __builtin_fmin(key, pack_key256(v, row[t])) : key;
+      }
+      key = row_min(key);
+      if (l == 0) red[R_KEY + wv] = key;
+    };
+    if (tid < NB) iamb[tid] = -1;
+    if (!done) publish_key();
+    __syncthreads();
+    while (!done && it < max_iter) {
+      ++it;
+      if (selecting) {
+        double kmin = red[R_KEY];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) kmin = __builtin_fmin(kmin, red[R_KEY + w]);
+        if (!(kmin < kBig)) {
+          status = QPB_OK;
+          break;
+        }
+        p = key_index256(kmin);
+        up = 0.0;
+        selecting = false;
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+          if (row[t] == p) {  // the four lanes of row p: u (permuted) and s_p
+            double *dst = ub + 32 * lk;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              *reinterpret_cast<double2 *>(&dst[4 * k]) = make_double2(E[t][k][0], E[t][k][1]);
+              *reinterpret_cast<double2 *>(&dst[4 * k + 2]) = make_double2(E[t][k][2], E[t][k][3]);
+            }
+            if (lk == 0) red[R_SP] = s[t];
+          }
+        __syncthreads();
+        double vr[RT];
+        row_dot(E, ub + 32 * lk, vr);  // v = D u: column p of G
+        if (lk == 0) {
+#pragma unroll
+          for (int t = 0; t < RT; ++t) vb[row[t]] = vr[t];
+        }
+        __syncthreads();
+      }
+      clk.tick(3);
+      // ---- r = G_WW^{-1} v[W] and the ratio test: slot t on thread t
+      if (wv < 2) {
+        const int t = tid;
+        double rt = 0.0, ratio = kBig;
+        if (t < hi) {
+          // four slots per round, all loads issued before the FMAs
+          double acc[4] = {0.0, 0.0, 0.0, 0.0};
+          int i = 0;
+          for (; i + 4 <= hi; i += 4) {
+            int c[4];
+            double gv[4], vv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              c[u] = iamb[i + u];
+              gv[u] = sym(Lp, t, i + u);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) vv[u] = vb[c[u] >= 0 ? c[u] : 0];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = __builtin_fma(gv[u], c[u] >= 0 ? vv[u] : 0.0, acc[u]);
+          }
+          for (; i < hi; ++i) {
+            const int c0 = iamb[i];
+            acc[0] = __builtin_fma(sym(Lp, t, i), c0 >= 0 ? vb[c0] : 0.0, acc[0]);
+          }
+          rt = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+          rb[t] = rt;
+          if (rt > 0.0 && iamb[t] >= 0) ratio = lamb[t] * rcp(rt);
+        }
+        const double wmin = wave_min(ratio);
+        // first slot reaching the minimum
+        const double kpos = wave_min((ratio == wmin && wmin < kBig) ? (double)t : 1e9);
+        if (l == 0) {
+          red[R_T1 + 2 * wv] = wmin;
+          red[R_T1 + 2 * wv + 1] = kpos;
+        }
+      }
+      __syncthreads();
+      clk.tick(4);
+      // ---- w = u - D_W^T r (permuted columns on threads 0..127), |w|^2
+      if (wv < 2) {
+        const int c = tid;
+        double wa[4] = {ub[c], 0.0, 0.0, 0.0};
+        const int ha = hi < QL ? hi : QL;
+        int j = 0;
+        for (; j + 4 <= ha; j += 4) {
+          double rr[4], dv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            rr[u] = rb[j + u];
+            dv[u] = DW.lds[(j + u) * NB + c];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) wa[u] = __builtin_fma(-rr[u], dv[u], wa[u]);
+        }
+        for (; j < ha; ++j) wa[0] = __builtin_fma(-rb[j], DW.lds[j * NB + c], wa[0]);
+        for (j = QL; j < hi; ++j) wa[1] = __builtin_fma(-rb[j], DW.gl[(j - QL) * NB + c], wa[1]);
+        const double w = (wa[0] + wa[1]) + (wa[2] + wa[3]);
+        wb[c] = w;
+        const double ws = wave_sum(w * w);
+        if (l == 0) red[R_ND2 + wv] = ws;
+      }
+      __syncthreads();
+      clk.tick(5);
+      // ---- step lengths (identical arithmetic on every wavefront)
+      const double nd2 = red[R_ND2] + red[R_ND2 + 1];
+      const double dd = vb[p];
+      const double sp = red[R_SP];
+      double t1 = kBig;
+      int kdrop = 0;
+      if (q > 0) {
+        const double m0 = red[R_T1], m1 = red[R_T1 + 2];
+        t1 = m0 <= m1 ? m0 : m1;
+        kdrop = (int)(m0 <= m1 ? red[R_T1 + 1] : red[R_T1 + 3]);
+      }
+      const double t2 = (nd2 > kDepTol * dd) ? -sp / nd2 : kBig;
+      const double tt = t1 < t2 ? t1 : t2;
+      if (!(tt < kBig)) {
+        status = QPB_INFEASIBLE;
+        break;
+      }
+      if (t2 < kBig) {
+        double ds[RT];
+        row_dot(E, wb + 32 * lk, ds);  // slack direction D w
+#pragma unroll
+        for (int t = 0; t < RT; ++t) s[t] = __builtin_fma(tt, ds[t], s[t]);
+      }
+      up += tt;
+      if (tid < hi) lamb[tid] = __builtin_fma(-tt, rb[tid], lamb[tid]);  // free slots: r = 0
+      if (t2 <= t1) {
+        // ---- ADD p in the lowest free slot a: G_WW^{-1} bordered
+        const int a = ~occ0 ? __builtin_ctzll(~occ0) : 64 + __builtin_ctzll(~occ1);
+        const int hn = a + 1 > hi ? a + 1 : hi;
+        const double inv = 1.0 / nd2;
+        for (int i = tid >> 3; i < hn; i += NT / 8) {
+          const double ri = rb[i];
+          for (int j = tid & 7; j <= i; j += 8) {
+            double &gij = Lp[tri(i, j)];
+            if (i == a) gij = j == a ? inv : -rb[j] * inv;
+            else if (j == a) gij = -ri * inv;
+            else if (i < hi) gij = __builtin_fma(ri * inv, rb[j], gij);
+          }
+        }
+        if (tid < NB) DW.row(a)[tid] = ub[tid];
+        if (tid == 0) {
+          iamb[a] = p;
+          lamb[a] = up;
+        }
+        if (a < 64) occ0 |= 1ull << a;
+        else occ1 |= 1ull << (a - 64);
+        hi = hn;
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+          if (row[t] == p) act[t] = true;
+        ++q;
+        selecting = true;
+      } else {
+        // ---- DROP slot k: Schur-complement downdate of G_WW^{-1} on the
+        // other slots, then row / column k cleared
+        const int k = kdrop;
+        const int cdrop = iamb[k];
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+          if (row[t] == cdrop) act[t] = false;
+        const double ikk = 1.0 / Lp[tri(k, k)];
+        for (int i = tid >> 3; i < hi; i += NT / 8) {
+          if (i == k) continue;
+          const double gik = sym(Lp, i, k) * ikk;
+          for (int j = tid & 7; j <= i; j += 8)
+            if (j != k) Lp[tri(i, j)] = __builtin_fma(-gik, sym(Lp, j, k), Lp[tri(i, j)]);
+        }
+        __syncthreads();
+        if (tid < hi) Lp[tid >= k ? tri(tid, k) : tri(k, tid)] = 0.0;
+        if (tid == 0) {
+          iamb[k] = -1;
+          lamb[k] = 0.0;
+        }
+        if (k < 64) occ0 &= ~(1ull << k);
+        else occ1 &= ~(1ull << (k - 64));
+        --q;
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+          if (row[t] == p && lk == 0) red[R_SP] = s[t];
+      }
+      if (selecting) publish_key();
+      __syncthreads();
+      clk.tick(6);
+    }
+
+    // ------------------------------------------------------------ outputs
+    // full multiplier vector by row (vb), the active-set words, g = y + D_W^T lam
+    for (int e = tid; e < MB; e += NT) vb[e] = 0.0;
+    __syncthreads();
+    if (tid < hi && iamb[tid] >= 0) vb[iamb[tid]] = lamb[tid];
+    if (tid < NB) {
+      double gsum = yb[tid];
+      const int ha = hi < QL ? hi : QL;
+      for (int j = 0; j < ha; ++j) gsum = __builtin_fma(lamb[j], DW.lds[j * NB + tid], gsum);
+      for (int j = QL; j < hi; ++j) gsum = __builtin_fma(lamb[j], DW.gl[(j - QL) * NB + tid], gsum);
+      yb[tid] = gsum;
+    }
+    {
+      uint32_t word = 0;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) word |= (uint32_t)(__ballot(act[t] && lk == 0) & 0xFFFFull) << (16 * t);
+      if (l == 0) flags[2 + wv] = (int)word;  // rows 32 wv .. 32 wv + 31
+    }
+    __syncthreads();
+    for (int e = tid; e < m; e += NT) lamg[g * m + e] = vb[e];
+    const int words = (m + 31) >> 5;
+    if (tid < words) actg[g * words + tid] = (uint32_t)flags[2 + tid];
+    // x = -L^{-T} g: L again (the triangle held G_WW^{-1})
+    bool finite = true;
+    clk.tick(7);
+    if (spd) {
+      for (int e = tid; e < tri(nb, 0); e += NT) Lp[e] = Lgl[e];
+      __syncthreads();
+      clk.tick(8);
+      if (wv == 0) {
+        double x0 = -yb[perm(l)], x1 = -yb[perm(l + 64)];
+        solve_upper(Lp, nb, l, x0, x1);
+        if (l < n) xg[g * n + l] = x0;
+        if (l + 64 < n) xg[g * n + l + 64] = x1;
+        const bool bad = (l < n && !(__builtin_fabs(x0) < kInf)) || (l + 64 < n && !(__builtin_fabs(x1) < kInf));
+        finite = __ballot(bad) == 0;
+      }
+    } else if (wv == 0) {
+      if (l < n) xg[g * n + l] = 0.0;
+      if (l + 64 < n) xg[g * n + l + 64] = 0.0;
+    }
+    if (tid == 0) {
+      statg[g] = (status == QPB_OK && !finite) ? QPB_NUMERICAL : status;
+      if (itg) itg[g] = it;
+    }
+    __syncthreads();
+    clk.tick(9);
+  }
+  if (threadIdx.x == 0) clk.flush(dbg);
+}
+
+}  // namespace gram
+}  // namespace qpb
+
+// scratch: per workgroup (NB - QL) D_W rows beyond the LDS ones + the queue head
+extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                         const double *b, double *x, double *lam, uint32_t *active,
+                                         int32_t *status, int32_t *iters, unsigned long long *sections,
+                                         hipStream_t stream) {
+  const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
+  const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const long long grid = d->batch < cus ? d->batch : cus;
+  const size_t rows_bytes = (size_t)grid * qpb::gram::SCRATCH * sizeof(double);
+  void *buf = nullptr;
+  e = hipMallocAsync(&buf, rows_bytes + 256, stream);
+  if (e != hipSuccess) return e;
+  int *queue = reinterpret_cast<int *>(static_cast<char *>(buf) + rows_bytes);
+  e = hipMemsetAsync(queue, 0, sizeof(int), stream);
+  if (e == hipSuccess) {
+    if (sections)
+      hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<true>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
+                         f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
+                         queue, static_cast<double *>(buf), sections);
+    else
+      hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<false>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
+                         f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
+                         queue, static_cast<double *>(buf), nullptr);
+    e = hipGetLastError();
+  }
+  const hipError_t e2 = hipFreeAsync(buf, stream);
+  return e != hipSuccess ? e : e2;
+}

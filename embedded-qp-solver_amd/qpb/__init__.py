@@ -43,6 +43,7 @@ MAX_N, MAX_M = 128, 256
 # qpb_desc.flags (include/qpb.h)
 FLAG_DIAG_L2, FLAG_DIAG_OCC2, FLAG_DIAG_PERSISTENT, FLAG_DIAG_MALL = 1, 4, 8, 16
 FLAG_MIXED, FLAG_DIAG_NO_REDO = 32, 64
+FLAG_DIAG_BLOCK = 128  # n <= 128 class: the round-1 kernel (qpb_gi_block.hip)
 STATUS_REDO = 100  # internal: a QP the mixed kernel leaves to the fp64 re-solve (FLAG_DIAG_NO_REDO only)
 
 

@@ -57,7 +57,7 @@ extern "C" {
 
 /* limits of this build's kernels: n <= 16, m <= 32 one QP per 16-lane DPP
  * row (qpb_gi.hip); n <= 32, m <= 64 one QP per wavefront (qpb_gi_wave.hip);
- * n <= 128, m <= 256 one QP per 1024-thread workgroup (qpb_gi_block.hip) */
+ * n <= 128, m <= 256 one QP per 1024-thread workgroup (qpb_gi_gram.hip) */
 #define QPB_MAX_N 128
 #define QPB_MAX_M 256
 
@@ -100,6 +100,11 @@ typedef enum qpb_error {
 /* diagnostic flag (with QPB_FLAG_MIXED): skip the fp64 re-solve; QPs that
  * would be re-solved keep status 100 (measures the re-solve fraction) */
 #define QPB_FLAG_DIAG_NO_REDO 64
+
+/* diagonal flag (32 < n <= 128 or 64 < m <= 256): the round-1 one-QP-per-
+ * workgroup kernel (qpb_gi_block.hip, G-I on a register-resident rotating D)
+ * instead of the Gram-form kernel (qpb_gi_gram.hip) -- kept for A/B runs */
+#define QPB_FLAG_DIAG_BLOCK 128
 
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */

@@ -1,5 +1,7 @@
-"""GPU parity of the one-QP-per-workgroup active-set kernel (qpb_gi_block.hip):
-32 < n <= 128, m <= 256, including BASELINE config 4's shape n=128, m=256.
+"""GPU parity of the one-QP-per-workgroup active-set kernel for the n <= 128
+class (qpb_gi_gram.hip; the round-1 kernel qpb_gi_block.hip behind
+QPB_FLAG_DIAG_BLOCK): 32 < n <= 128, m <= 256, including BASELINE configs[3]'s
+shape n=128, m=256.
 Oracle: oracle.active_set_solve (KKT-certified primal active set) per QP;
 x within 1e-6 relative, active set bit-exact, multipliers within 1e-6, and the
 KKT certificate on every GPU answer.  Calls go through the C-ABI."""
@@ -22,9 +24,9 @@ def qpb():
     return q
 
 
-def _solve(qpb, H, f, A=None, b=None):
+def _solve(qpb, H, f, A=None, b=None, flags=0):
     dev = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in ((H, f) if A is None else (H, f, A, b))]
-    sol = qpb.solve(*dev)
+    sol = qpb.solve(*dev, flags=flags)
     torch.cuda.synchronize()
     return [t.cpu().numpy() for t in sol]
 
@@ -57,15 +59,37 @@ def test_block_kernel_unconstrained(qpb):
     assert _relerr(x, np.linalg.solve(H, -f[..., None])[..., 0]).max() <= 1e-9
 
 
-def test_block_kernel_config4_batch(qpb):
-    """BASELINE config 4 shape at a moderate batch from the on-device
-    generator: every QP KKT-certified."""
-    B = 512
-    H, f, A, b = qpb.generate(128, B, 20261015, family="box")
+def test_round1_block_kernel_still_agrees(qpb):
+    """The round-1 kernel (QPB_FLAG_DIAG_BLOCK, kept for A/B runs) on one shape."""
+    H, f, A, b = O.family_conditioned(2000 + 48 + 96, 4, 48, m=96, box=10.0, kind="box")
+    x, lam, act, st, it = _solve(qpb, H, f, A, b, flags=qpb.FLAG_DIAG_BLOCK)
+    x2, lam2, act2, st2, it2 = _solve(qpb, H, f, A, b)
+    assert (st == qpb.OK).all() and (st2 == qpb.OK).all()
+    assert np.abs(x - x2).max() <= 1e-9 * max(1.0, np.abs(x2).max())
+    assert np.array_equal(act, act2)
+
+
+@pytest.mark.parametrize("kind", ["box", "dense"])
+def test_config3_full_batch(qpb, kind):
+    """BASELINE configs[3] as specified (n=128, m=256, B=16384) from the
+    on-device generator: every QP KKT-certified, 32 QPs against the oracle."""
+    B = 16384
+    H, f, A, b = qpb.generate(128, B, 20261015, family=kind)
     sol = qpb.solve(H, f, A, b)
     torch.cuda.synchronize()
     st = sol.status.cpu().numpy()
     assert (st == qpb.OK).all(), np.bincount(st)
-    Hn, fn, An, bn = (t.cpu().numpy() for t in (H, f, A, b))
-    r = O.kkt_residuals(Hn, fn, An, bn, sol.x.cpu().numpy(), sol.lam.cpu().numpy())
-    assert max(float(v.max()) for v in r.values()) <= 1e-9
+    x, lam = sol.x.cpu().numpy(), sol.lam.cpu().numpy()
+    mask = qpb.active_mask_to_bool(sol.active.cpu().numpy(), 256)
+    for k0 in range(0, B, 2048):  # KKT on every QP, in host-memory-sized chunks
+        sl = slice(k0, k0 + 2048)
+        Hn, fn, An, bn = (t[sl].cpu().numpy() for t in (H, f, A, b))
+        r = O.kkt_residuals(Hn, fn, An, bn, x[sl], lam[sl])
+        assert max(float(v.max()) for v in r.values()) <= 1e-9, (k0, {k: float(v.max()) for k, v in r.items()})
+    idx = np.linspace(0, B - 1, 32).astype(int)
+    Hn, fn, An, bn = (t[idx].cpu().numpy() for t in (H, f, A, b))
+    for j, i in enumerate(idx):
+        ref = O.active_set_solve(Hn[j], fn[j], An[j], bn[j])
+        assert ref.status == 0
+        assert _relerr(x[i:i + 1], ref.x[None]).max() <= X_TOL, i
+        assert np.array_equal(mask[i], ref.active), i
