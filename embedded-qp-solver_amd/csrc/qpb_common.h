@@ -213,7 +213,7 @@ __device__ __forceinline__ int wave_max4(int v) {
 
 // Diagnostic builds only (STAMP = true, qpb_solve_sections): s_memrealtime stamps
 // (100 MHz) accumulate each wave's ticks per kernel section; the real kernels have none.
-constexpr int kSections = 12;
+constexpr int kSections = 20;
 template <bool ON>
 struct SectionClock {
   __device__ __forceinline__ void tick(int) {}

@@ -52,27 +52,30 @@ constexpr int NWV = NT / 64;
 constexpr int RT = MB / 16 / NWV;  // 16-row tiles of D per wavefront (2)
 constexpr int LP = NB * (NB + 1) / 2;  // packed triangle, 8256 doubles
 constexpr int LDS_D = 20480;           // 160 KiB
-constexpr int NBUF = 1024;
+constexpr int PV = 4 * 34;  // a padded permuted vector (see pad())
+constexpr int NBUF = 2008;
 constexpr int OFF_TRI = 0;
 constexpr int OFF_ROWS = LP;  // diagonal-tile inverses (setup) / D_W rows (loop)
 constexpr int OFF_BUF = LDS_D - NBUF;
-constexpr int QL = (OFF_BUF - OFF_ROWS) / NB;  // D_W rows in LDS (87)
-constexpr int B_U = OFF_BUF;                   // u = D[p,:] (permuted column order)
-constexpr int B_W = B_U + NB;                  // w (permuted)
-constexpr int B_V = B_W + NB;                  // v = D u (by row); lambda scatter at the end
-constexpr int B_R = B_V + MB;                  // r by active position
-constexpr int B_LAM = B_R + NB;                // multipliers by active position
-constexpr int B_Y = B_LAM + NB;                // y (permuted), then y + D_W^T lam
-constexpr int B_RED = B_Y + NB;                // selection keys, partial reductions, scalars
-constexpr int B_INT = B_RED + 32;              // ints: flags, queue slot, mask halves (64)
-constexpr int B_IAM = B_INT + 32;              // ints: constraint index by position (128)
+constexpr int QL = (OFF_BUF - OFF_ROWS) / NB;  // D_W rows in LDS (79)
+// Permuted vectors (u, w, y) keep lane group g's 32 entries at 34 g: the four
+// groups' b128 reads then start 4 banks apart instead of on the same banks.
+constexpr int B_CAND = OFF_BUF;                // per wave: its most violated row of D (PV each)
+constexpr int B_CSP = B_CAND + NWV * PV;       // per wave: that row's slack
+constexpr int B_W = B_CSP + NWV;               // w (padded permuted)
+constexpr int B_V = B_W + PV;                  // v = D u (by row); lambda scatter at the end
+constexpr int B_R = B_V + MB;                  // r by slot
+constexpr int B_LAM = B_R + NB;                // multipliers by slot
+constexpr int B_Y = B_LAM + NB;                // y (padded permuted), then y + D_W^T lam
+constexpr int B_RED = B_Y + PV;                // selection keys, partial reductions, scalars
+constexpr int B_INT = B_RED + 32;              // ints: flags, queue slot, mask words (64)
+constexpr int B_IAM = B_INT + 32;              // ints: constraint index by slot (128)
 static_assert(B_IAM + 64 == LDS_D, "LDS layout");
 static_assert(OFF_ROWS + 8 * 256 <= OFF_BUF, "diagonal-tile inverses fit the row area");
 // B_RED slots
 constexpr int R_KEY = 0;    // per-wave selection keys (NWV)
-constexpr int R_T1 = 16;    // 2 per-wave (ratio min, argmin position)
-constexpr int R_ND2 = 20;   // 2 per-wave partial |w|^2
-constexpr int R_SP = 22;    // s_p
+constexpr int R_T1 = 8;     // per-wave (ratio min, argmin slot) pairs (2 NWV)
+constexpr int R_ND2 = 24;   // per-wave partial |w|^2 (NWV)
 constexpr double kDepTol = 1e-24;
 constexpr long long SCRATCH = LP + (long long)(NB - QL) * NB;  // doubles per workgroup
 
@@ -82,6 +85,8 @@ __device__ __forceinline__ int tri(int i, int j) { return ((i * (i + 1)) >> 1) +
 // column c -> its place in the permuted vector layout (lane group c & 3 reads
 // a contiguous 32-double block in the order of its registers)
 __device__ __forceinline__ int perm(int c) { return ((c & 3) << 5) + ((c >> 4) << 2) + ((c >> 2) & 3); }
+// a permuted index 0..127 -> its slot in the padded layout
+__device__ __forceinline__ int pad(int c) { return c + 2 * (c >> 5); }
 __device__ __forceinline__ double mfma(double a, double b, d4 &c) {
   c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
   return 0.0;
@@ -162,16 +167,39 @@ __device__ __forceinline__ double sym(const double *P, int i, int j) { return i 
 // row i, pivot rows by DPP broadcast as in qpb_gi.hip) and inverted (lane j
 // solves column j); the panel below it is multiplied by that inverse and the
 // trailing tiles updated on the matrix cores.  Returns false if a pivot <= 0.
-__device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__ Hq, int n, int T) {
+template <class CLK>
+__device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__ Hq, int n, int T, int tid, CLK &clk) {
   double *Lp = lds + OFF_TRI;
   double *LI = lds + OFF_ROWS;
   int *flags = reinterpret_cast<int *>(lds + B_INT);
-  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int l = tid & 63, wv = tid >> 6;  // tid: the caller's opaque thread id
   const int nb = 16 * T;
-  for (int r = wv; r < nb; r += NWV)  // row r, lanes along the columns (coalesced)
-    for (int c = l; c <= r; c += 64) Lp[tri(r, c)] = (r < n) ? Hq[r * n + c] : (r == c ? 1.0 : 0.0);
+  {
+    // rows wv, wv + 8, ... (lanes along the columns: coalesced); every load
+    // is issued before the first store, one HBM round trip per QP
+    double h[NB / NWV][2];
+#pragma unroll
+    for (int u = 0; u < NB / NWV; ++u) {
+      const int r = wv + NWV * u;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int c = l + 64 * h2;
+        h[u][h2] = (r < n && c <= r) ? Hq[r * n + c] : (r == c ? 1.0 : 0.0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NB / NWV; ++u) {
+      const int r = wv + NWV * u;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int c = l + 64 * h2;
+        if (r < nb && c <= r) Lp[tri(r, c)] = h[u][h2];
+      }
+    }
+  }
   if (tid == 0) flags[0] = 0;
   __syncthreads();
+  clk.tick(11);
   for (int K = 0; K < T; ++K) {
     if (wv == 0) {
       int i = l & 15;
@@ -193,7 +221,7 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
         // entries, broadcast by DPP
         const double akk = bc<k>(a[k]);
         ok = ok && (akk > 0.0);
-        const double ik = rsq(akk);
+        const double ik = rsq1(akk);  // hardware estimate + one Newton step (qpb_common.h)
         const double ik2 = ik * ik;
         const double c = a[k] * ik2;
         const double ne2 = -(e[k] * ik2);
@@ -209,7 +237,6 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
           pin(a[j]);
         });
         a[k] *= ik;
-        __builtin_amdgcn_sched_barrier(0);
       });
       if (l < 16) {
 #pragma unroll
@@ -221,6 +248,7 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
       if (l == 0 && !ok) flags[0] = 1;
     }
     __syncthreads();
+    clk.tick(12);
     // panel: L[I, K] = H~[I, K] Linv_K^T, one tile per wavefront
     const int li = l & 15, lk = l >> 4;
     if (wv < T - K - 1) {
@@ -233,31 +261,48 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
       for (int r = 0; r < 4; ++r) Lp[tri(16 * I + lk + 4 * r, 16 * K + li)] = acc[r];
     }
     __syncthreads();
+    clk.tick(13);
     // trailing tiles (I, J), K < J <= I < T, round robin over the wavefronts
     const int nr = T - K - 1, ntile = nr * (nr + 1) / 2;
-    for (int t = wv; t < ntile; t += NWV) {
-      int I = (int)((__builtin_sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-      if (tri(I + 1, 0) <= t) ++I;
-      if (tri(I, 0) > t) --I;
-      int J = t - tri(I, 0);
-      I += K + 1;
-      J += K + 1;
-      d4 acc;
+    // two tiles per wavefront at a time: two independent MFMA chains
+    for (int t0 = wv; t0 < ntile; t0 += 2 * NWV) {
+      int I[2], J[2];
+      bool on[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * I + lk + 4 * r, col = 16 * J + li;
-        acc[r] = row >= col ? Lp[tri(row, col)] : 0.0;
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int t = t0 + NWV * h2;
+        on[h2] = t < ntile;
+        const int tt = on[h2] ? t : t0;
+        int i = (int)((__builtin_sqrt(8.0 * tt + 1.0) - 1.0) * 0.5);
+        if (tri(i + 1, 0) <= tt) ++i;
+        if (tri(i, 0) > tt) --i;
+        J[h2] = tt - tri(i, 0) + K + 1;
+        I[h2] = i + K + 1;
       }
+      d4 acc[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * I[h2] + lk + 4 * r, col = 16 * J[h2] + li;
+          acc[h2][r] = row >= col ? Lp[tri(row, col)] : 0.0;
+        }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        mfma(-Lp[tri(16 * I + li, 16 * K + 4 * s + lk)], Lp[tri(16 * J + li, 16 * K + 4 * s + lk)], acc);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * I + lk + 4 * r, col = 16 * J + li;
-        if (row >= col) Lp[tri(row, col)] = acc[r];
-      }
+        for (int h2 = 0; h2 < 2; ++h2)
+          mfma(-Lp[tri(16 * I[h2] + li, 16 * K + 4 * s + lk)], Lp[tri(16 * J[h2] + li, 16 * K + 4 * s + lk)],
+               acc[h2]);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * I[h2] + lk + 4 * r, col = 16 * J[h2] + li;
+          if (on[h2] && row >= col) Lp[tri(row, col)] = acc[h2][r];
+        }
     }
     __syncthreads();
+    clk.tick(14);
   }
   return flags[0] == 0;
 }
@@ -347,7 +392,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
   SectionClock<STAMP> clk;
   double *Lp = lds + OFF_TRI;  // L, then G_WW^{-1} (packed lower)
   double *LI = lds + OFF_ROWS;
-  double *ub = lds + B_U, *wb = lds + B_W, *vb = lds + B_V, *rb = lds + B_R, *lamb = lds + B_LAM, *yb = lds + B_Y;
+  double *wb = lds + B_W, *vb = lds + B_V, *rb = lds + B_R, *lamb = lds + B_LAM, *yb = lds + B_Y;
   double *red = lds + B_RED;
   int *flags = reinterpret_cast<int *>(lds + B_INT);
   int *iamb = reinterpret_cast<int *>(lds + B_IAM);
@@ -355,6 +400,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
   double *Lgl = scratch + (long long)blockIdx.x * SCRATCH;
   const Rows DW{lds + OFF_ROWS, Lgl + LP};
   const int T = (n + 15) >> 4, nb = 16 * T;
+  bool first = true;
   for (;;) {
     // lane ids re-derived opaquely per QP: lane-dependent values are not
     // hoisted out of the QP loop (they would stay live across it)
@@ -369,16 +415,22 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       row[t] = 16 * (RT * wv + t) + li;
       rowok[t] = row[t] < m;
     }
-    if (tid == 0) flags[1] = atomicAdd(queue, 1);
+    // the queue is read one QP ahead: the next QP's inputs are pulled into
+    // the caches while this one iterates (see the prefetch below)
+    if (tid == 0) {
+      flags[1] = first ? atomicAdd(queue, 1) : flags[30];
+      flags[30] = atomicAdd(queue, 1);
+    }
+    first = false;
     __syncthreads();
-    const long long g = flags[1];
+    const long long g = flags[1], gnext = flags[30];
     if (g >= batch) break;
     const double *Hq = Hg + g * (long long)n * n;
     const double *Aq = Ag + g * (long long)m * n;
 
     // ------------------------------------------------------------ setup
     clk.tick(10);
-    const bool spd = cholesky(lds, Hq, n, T);
+    const bool spd = cholesky(lds, Hq, n, T, tid, clk);
 #ifdef GRAM_ONLY_CHOL
     if (tid == 0) statg[g] = spd;
     continue;
@@ -392,8 +444,8 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     if (wv == 0) {
       double a0 = l < n ? fg[g * n + l] : 0.0, a1 = l + 64 < n ? fg[g * n + l + 64] : 0.0;
       solve_lower(Lp, nb, l, a0, a1);
-      yb[perm(l)] = a0;
-      yb[perm(l + 64)] = a1;
+      yb[pad(perm(l))] = a0;
+      yb[pad(perm(l + 64))] = a1;
     }
 
     // D = A L^{-T} on the matrix cores: tile k of D^T (16 columns of D x 16
@@ -457,7 +509,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     if (zero_bad && lk == 0) flags[20] = 1;
     {
       double dy[RT];
-      row_dot(E, yb + 32 * lk, dy);  // s = b + D y
+      row_dot(E, yb + 34 * lk, dy);  // s = b + D y
 #pragma unroll
       for (int t = 0; t < RT; ++t) s[t] = bl[t] + dy[t];
     }
@@ -465,6 +517,22 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     int status = !spd ? QPB_NOT_SPD : (flags[20] ? QPB_INFEASIBLE : QPB_MAX_ITER);
     bool done = status != QPB_MAX_ITER;
     clk.tick(2);
+    // one dword of every 128-byte line of the next QP's H and A: the lines
+    // reach L2 / the Infinity Cache during this QP's iterations (HBM is idle
+    // then); the values are only consumed after the loop
+    constexpr int PF = 6;
+    uint32_t pf[PF];
+    {
+      const long long gn = gnext < batch ? gnext : g;
+      const uint32_t *hn = reinterpret_cast<const uint32_t *>(Hg + gn * (long long)n * n);
+      const uint32_t *an = reinterpret_cast<const uint32_t *>(Ag + gn * (long long)m * n);
+      const int lh = (n * n + 15) >> 4, la = (m * n + 15) >> 4;  // 128-byte lines
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int line = tid + NT * u;
+        pf[u] = line < lh ? hn[32 * line] : (line - lh < la ? an[32 * (line - lh)] : 0u);
+      }
+    }
 
     // ------------------------------------------------------- active set
     // The active constraints live in SLOTS (0 .. hi-1, occupancy mask occ):
@@ -473,19 +541,37 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     // may run over every slot below hi).  A DROP frees a slot, an ADD takes
     // the lowest free one: nothing is ever shifted.  Row i of the packed
     // inverse belongs to threads 8 (i mod NT/8) + c, columns c, c + 8, ...
-    int q = 0, it = 0, p = 0, hi = 0;
+    int it = 0, p = 0, hi = 0;
     unsigned long long occ0 = 0, occ1 = 0;  // slot occupancy (uniform)
     bool selecting = true;
     double up = 0.0;
+    const double *ub = lds + B_CAND;  // u = D[p,:]: the winning wave's candidate row
+    // each wave offers its most violated row: the key (normalised slack, row
+    // in the low mantissa bits), the row of D (padded permuted) and its slack,
+    // so the next selection needs no broadcast round of its own
     auto publish_key = [&]() {
       double key = kBig;
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
         const double v = s[t] * invn[t];
-        key = (lk == 0 && !act[t] && v < thr[t]) ? __builtin_fmin(key, pack_key256(v, row[t])) : key;
+        key = (!act[t] && v < thr[t]) ? __builtin_fmin(key, pack_key256(v, row[t])) : key;
       }
-      key = row_min(key);
+      key = row_min(key);  // the 16 rows of each tile pair, on every lane group
       if (l == 0) red[R_KEY + wv] = key;
+      const int pw = key_index256(key);
+      if (key < kBig) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+          if (row[t] == pw) {  // the four lanes of the candidate row
+            double *dst = lds + B_CAND + wv * PV + 34 * lk;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              *reinterpret_cast<double2 *>(&dst[4 * k]) = make_double2(E[t][k][0], E[t][k][1]);
+              *reinterpret_cast<double2 *>(&dst[4 * k + 2]) = make_double2(E[t][k][2], E[t][k][3]);
+            }
+            if (lk == 0) lds[B_CSP + wv] = s[t];
+          }
+      }
     };
     if (tid < NB) iamb[tid] = -1;
     if (!done) publish_key();
@@ -501,22 +587,11 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           break;
         }
         p = key_index256(kmin);
+        ub = lds + B_CAND + (p / (16 * RT)) * PV;
         up = 0.0;
         selecting = false;
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-          if (row[t] == p) {  // the four lanes of row p: u (permuted) and s_p
-            double *dst = ub + 32 * lk;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              *reinterpret_cast<double2 *>(&dst[4 * k]) = make_double2(E[t][k][0], E[t][k][1]);
-              *reinterpret_cast<double2 *>(&dst[4 * k + 2]) = make_double2(E[t][k][2], E[t][k][3]);
-            }
-            if (lk == 0) red[R_SP] = s[t];
-          }
-        __syncthreads();
         double vr[RT];
-        row_dot(E, ub + 32 * lk, vr);  // v = D u: column p of G
+        row_dot(E, ub + 34 * lk, vr);  // v = D u: column p of G
         if (lk == 0) {
 #pragma unroll
           for (int t = 0; t < RT; ++t) vb[row[t]] = vr[t];
@@ -524,38 +599,28 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         __syncthreads();
       }
       clk.tick(3);
-      // ---- r = G_WW^{-1} v[W] and the ratio test: slot t on thread t
-      if (wv < 2) {
-        const int t = tid;
-        double rt = 0.0, ratio = kBig;
+      // ---- r = G_WW^{-1} v[W] and the ratio test on every wavefront: lane
+      // (g, j) of wave w takes slot t = 16 w + j over the columns i = g mod 4
+      // (group sums finish the dot products)
+      {
+        const int t = 16 * wv + li;
+        double acc0 = 0.0, acc1 = 0.0;
+        for (int i = lk; i < hi; i += 8) {
+          const bool two = i + 4 < hi;
+          const int c0 = iamb[i], c2 = two ? iamb[i + 4] : -1;
+          const double g0 = sym(Lp, t, i), g2 = two ? sym(Lp, t, i + 4) : 0.0;
+          acc0 = __builtin_fma(g0, c0 >= 0 ? vb[c0] : 0.0, acc0);
+          acc1 = __builtin_fma(g2, c2 >= 0 ? vb[c2] : 0.0, acc1);
+        }
+        const double rt = group_sum(acc0 + acc1);
+        double ratio = kBig;
         if (t < hi) {
-          // four slots per round, all loads issued before the FMAs
-          double acc[4] = {0.0, 0.0, 0.0, 0.0};
-          int i = 0;
-          for (; i + 4 <= hi; i += 4) {
-            int c[4];
-            double gv[4], vv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              c[u] = iamb[i + u];
-              gv[u] = sym(Lp, t, i + u);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) vv[u] = vb[c[u] >= 0 ? c[u] : 0];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] = __builtin_fma(gv[u], c[u] >= 0 ? vv[u] : 0.0, acc[u]);
-          }
-          for (; i < hi; ++i) {
-            const int c0 = iamb[i];
-            acc[0] = __builtin_fma(sym(Lp, t, i), c0 >= 0 ? vb[c0] : 0.0, acc[0]);
-          }
-          rt = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-          rb[t] = rt;
+          if (lk == 0) rb[t] = rt;
           if (rt > 0.0 && iamb[t] >= 0) ratio = lamb[t] * rcp(rt);
         }
-        const double wmin = wave_min(ratio);
+        const double wmin = row_min(ratio);  // the wave's 16 slots (every row holds them)
         // first slot reaching the minimum
-        const double kpos = wave_min((ratio == wmin && wmin < kBig) ? (double)t : 1e9);
+        const double kpos = row_min((ratio == wmin && wmin < kBig) ? (double)t : 1e9);
         if (l == 0) {
           red[R_T1 + 2 * wv] = wmin;
           red[R_T1 + 2 * wv + 1] = kpos;
@@ -563,55 +628,63 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       }
       __syncthreads();
       clk.tick(4);
-      // ---- w = u - D_W^T r (permuted columns on threads 0..127), |w|^2
-      if (wv < 2) {
-        const int c = tid;
-        double wa[4] = {ub[c], 0.0, 0.0, 0.0};
+      // ---- w = u - D_W^T r: lane (g, j) of wave w takes (permuted) column
+      // 16 w + j over the slots j' = g mod 4; |w|^2 per wave
+      {
+        const int c = 16 * wv + li;
+        double acc0 = 0.0, acc1 = 0.0;
         const int ha = hi < QL ? hi : QL;
-        int j = 0;
-        for (; j + 4 <= ha; j += 4) {
-          double rr[4], dv[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            rr[u] = rb[j + u];
-            dv[u] = DW.lds[(j + u) * NB + c];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) wa[u] = __builtin_fma(-rr[u], dv[u], wa[u]);
+        int j = lk;
+        for (; j + 4 < ha; j += 8) {
+          acc0 = __builtin_fma(-rb[j], DW.lds[j * NB + c], acc0);
+          acc1 = __builtin_fma(-rb[j + 4], DW.lds[(j + 4) * NB + c], acc1);
         }
-        for (; j < ha; ++j) wa[0] = __builtin_fma(-rb[j], DW.lds[j * NB + c], wa[0]);
-        for (j = QL; j < hi; ++j) wa[1] = __builtin_fma(-rb[j], DW.gl[(j - QL) * NB + c], wa[1]);
-        const double w = (wa[0] + wa[1]) + (wa[2] + wa[3]);
-        wb[c] = w;
-        const double ws = wave_sum(w * w);
+        if (j < ha) acc0 = __builtin_fma(-rb[j], DW.lds[j * NB + c], acc0);
+        for (j = QL + lk; j < hi; j += 4) acc1 = __builtin_fma(-rb[j], DW.gl[(j - QL) * NB + c], acc1);
+        const double uc = ub[pad(c)];
+        const double w = uc + group_sum(acc0 + acc1);
+        if (lk == 0) {
+          wb[pad(c)] = w;
+          // u into the D_W row of the slot an ADD would take (harmless if this
+          // step turns out a DROP: a free slot's r is 0); the candidate rows
+          // are rewritten in the step phase
+          const int anext = ~occ0 ? __builtin_ctzll(~occ0) : 64 + __builtin_ctzll(~occ1);
+          DW.row(anext)[c] = uc;
+        }
+        const double ws = wave_sum(lk == 0 ? w * w : 0.0);
         if (l == 0) red[R_ND2 + wv] = ws;
       }
       __syncthreads();
       clk.tick(5);
       // ---- step lengths (identical arithmetic on every wavefront)
-      const double nd2 = red[R_ND2] + red[R_ND2 + 1];
+      double nd2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) nd2 += red[R_ND2 + w];
       const double dd = vb[p];
-      const double sp = red[R_SP];
+      const double sp = lds[B_CSP + p / (16 * RT)];
       double t1 = kBig;
       int kdrop = 0;
-      if (q > 0) {
-        const double m0 = red[R_T1], m1 = red[R_T1 + 2];
-        t1 = m0 <= m1 ? m0 : m1;
-        kdrop = (int)(m0 <= m1 ? red[R_T1 + 1] : red[R_T1 + 3]);
-      }
+#pragma unroll
+      for (int w = 0; w < NWV; ++w)  // waves in slot order: ties keep the lowest slot
+        if (red[R_T1 + 2 * w] < t1) {
+          t1 = red[R_T1 + 2 * w];
+          kdrop = (int)red[R_T1 + 2 * w + 1];
+        }
       const double t2 = (nd2 > kDepTol * dd) ? -sp / nd2 : kBig;
       const double tt = t1 < t2 ? t1 : t2;
       if (!(tt < kBig)) {
         status = QPB_INFEASIBLE;
         break;
       }
+      clk.tick(15);
       if (t2 < kBig) {
         double ds[RT];
-        row_dot(E, wb + 32 * lk, ds);  // slack direction D w
+        row_dot(E, wb + 34 * lk, ds);  // slack direction D w
 #pragma unroll
         for (int t = 0; t < RT; ++t) s[t] = __builtin_fma(tt, ds[t], s[t]);
       }
       up += tt;
+      clk.tick(16);
       if (tid < hi) lamb[tid] = __builtin_fma(-tt, rb[tid], lamb[tid]);  // free slots: r = 0
       if (t2 <= t1) {
         // ---- ADD p in the lowest free slot a: G_WW^{-1} bordered
@@ -627,7 +700,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
             else if (i < hi) gij = __builtin_fma(ri * inv, rb[j], gij);
           }
         }
-        if (tid < NB) DW.row(a)[tid] = ub[tid];
         if (tid == 0) {
           iamb[a] = p;
           lamb[a] = up;
@@ -638,7 +710,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 #pragma unroll
         for (int t = 0; t < RT; ++t)
           if (row[t] == p) act[t] = true;
-        ++q;
         selecting = true;
       } else {
         // ---- DROP slot k: Schur-complement downdate of G_WW^{-1} on the
@@ -663,27 +734,30 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         }
         if (k < 64) occ0 &= ~(1ull << k);
         else occ1 &= ~(1ull << (k - 64));
-        --q;
 #pragma unroll
-        for (int t = 0; t < RT; ++t)
-          if (row[t] == p && lk == 0) red[R_SP] = s[t];
+        for (int t = 0; t < RT; ++t)  // p stays selected: its slack after the partial step
+          if (row[t] == p && lk == 0) lds[B_CSP + wv] = s[t];
       }
+      clk.tick(17);
       if (selecting) publish_key();
+      clk.tick(18);
       __syncthreads();
       clk.tick(6);
     }
 
+#pragma unroll
+    for (int u = 0; u < PF; ++u) asm volatile("" ::"v"(pf[u]));
     // ------------------------------------------------------------ outputs
     // full multiplier vector by row (vb), the active-set words, g = y + D_W^T lam
     for (int e = tid; e < MB; e += NT) vb[e] = 0.0;
     __syncthreads();
     if (tid < hi && iamb[tid] >= 0) vb[iamb[tid]] = lamb[tid];
     if (tid < NB) {
-      double gsum = yb[tid];
+      double gsum = yb[pad(tid)];
       const int ha = hi < QL ? hi : QL;
       for (int j = 0; j < ha; ++j) gsum = __builtin_fma(lamb[j], DW.lds[j * NB + tid], gsum);
       for (int j = QL; j < hi; ++j) gsum = __builtin_fma(lamb[j], DW.gl[(j - QL) * NB + tid], gsum);
-      yb[tid] = gsum;
+      yb[pad(tid)] = gsum;
     }
     {
       uint32_t word = 0;
@@ -703,7 +777,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       __syncthreads();
       clk.tick(8);
       if (wv == 0) {
-        double x0 = -yb[perm(l)], x1 = -yb[perm(l + 64)];
+        double x0 = -yb[pad(perm(l))], x1 = -yb[pad(perm(l + 64))];
         solve_upper(Lp, nb, l, x0, x1);
         if (l < n) xg[g * n + l] = x0;
         if (l + 64 < n) xg[g * n + l + 64] = x1;

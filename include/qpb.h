@@ -168,7 +168,7 @@ int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
 
 /* Diagnostic: same solve (n = 16 with 16 < m <= 32, or 16 < n <= 32 with
  * m <= 64) by a build of the kernel with s_memrealtime stamps (100 MHz); adds
- * each wavefront's ticks per kernel section into sections[] (12 counters).
+ * each wavefront's ticks per kernel section into sections[] (20 counters).
  * n = 16: load, cholesky, substitution, init, select, exchange, back-solve,
  * step, add, drop, loop-exit, output.  16 < n <= 32: load, sweep, init,
  * select, exchange, back-solve, step, add, drop, loop-exit, x, stores. */

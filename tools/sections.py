@@ -25,7 +25,7 @@ out = {}
 for fam, n, B in cases:
     H, f, A, b = qpb.generate(n, B, 20261015, family=fam)
     sol = qpb.solve(H, f, A, b)
-    sec = torch.zeros(12, dtype=torch.int64, device=dev)
+    sec = torch.zeros(20, dtype=torch.int64, device=dev)
     qpb.solve_sections(H, f, A, b, sec, out=sol)
     sec.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
