@@ -53,7 +53,7 @@ constexpr int RT = MB / 16 / NWV;  // 16-row tiles of D per wavefront (2)
 constexpr int LP = NB * (NB + 1) / 2;  // packed triangle, 8256 doubles
 constexpr int LDS_D = 20480;           // 160 KiB
 constexpr int PV = 4 * 34;  // a padded permuted vector (see pad())
-constexpr int NBUF = 2008;
+constexpr int NBUF = 2136;
 constexpr int OFF_TRI = 0;
 constexpr int OFF_ROWS = LP;  // diagonal-tile inverses (setup) / D_W rows (loop)
 constexpr int OFF_BUF = LDS_D - NBUF;
@@ -65,7 +65,8 @@ constexpr int B_CSP = B_CAND + NWV * PV;       // per wave: that row's slack
 constexpr int B_W = B_CSP + NWV;               // w (padded permuted)
 constexpr int B_V = B_W + PV;                  // v = D u (by row); lambda scatter at the end
 constexpr int B_R = B_V + MB;                  // r by slot
-constexpr int B_LAM = B_R + NB;                // multipliers by slot
+constexpr int B_CB = B_R + NB;                 // c = v[W] by slot
+constexpr int B_LAM = B_CB + NB;               // multipliers by slot
 constexpr int B_Y = B_LAM + NB;                // y (padded permuted), then y + D_W^T lam
 constexpr int B_RED = B_Y + PV;                // selection keys, partial reductions, scalars
 constexpr int B_INT = B_RED + 32;              // ints: flags, queue slot, mask words (64)
@@ -200,57 +201,84 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
   if (tid == 0) flags[0] = 0;
   __syncthreads();
   clk.tick(11);
-  for (int K = 0; K < T; ++K) {
-    if (wv == 0) {
-      int i = l & 15;
-      asm volatile("" : "+v"(i));  // opaque per step: nothing lane-dependent is hoisted and kept live
-      const int r0 = 16 * K;
-      // lane i: row i of the tile (a, the full symmetric row) and row i of
-      // the identity (e): the sweep turns e into row i of L^{-T}, i.e.
-      // column i of the tile inverse, alongside the factorisation
-      double a[16], e[16];
+  // the diagonal tile K, on wavefront 0
+  auto factor_diag = [&](int K) {
+    int i = l & 15;
+    asm volatile("" : "+v"(i));  // opaque per step: nothing lane-dependent is hoisted and kept live
+    const int r0 = 16 * K;
+    // lane i: row i of the tile (a, the full symmetric row) and row i of
+    // the identity (e): the sweep turns e into row i of L^{-T}, i.e.
+    // column i of the tile inverse, alongside the factorisation
+    double a[16], e[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      a[j] = j <= i ? Lp[tri(r0 + i, r0 + j)] : Lp[tri(r0 + j, r0 + i)];
+      e[j] = j == i ? 1.0 : 0.0;
+    }
+    bool ok = true;
+    unroll<16>([&](auto Kc) {
+      constexpr int k = Kc;
+      // pivot row k of the Schur complement = column k (symmetry): lane k's
+      // entries, broadcast by DPP
+      const double akk = bc<k>(a[k]);
+      ok = ok && (akk > 0.0);
+      const double ik = rsq1(akk);  // hardware estimate + one Newton step (qpb_common.h)
+      const double ik2 = ik * ik;
+      const double c = a[k] * ik2;
+      const double ne2 = -(e[k] * ik2);
+      e[k] *= ik;
+      const double nc = -c;
+      // broadcasts fused into v_fmac_f64_dpp (the pivot row read straight
+      // from lane k); the e update reads lane k's a[j] before the a update of
+      // the same j writes it (volatile asm keeps the order); a[j] was last
+      // written in the previous step, well over two instructions before (the
+      // DPP read hazard)
+      unroll<15 - k>([&](auto J) {
+        constexpr int j = k + 1 + J;
+        fmac_bc<k>(e[j], a[j], ne2);
+        fmac_bc<k>(a[j], a[j], nc);
+      });
+      a[k] *= ik;
+    });
+    if (l < 16) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        a[j] = j <= i ? Lp[tri(r0 + i, r0 + j)] : Lp[tri(r0 + j, r0 + i)];
-        e[j] = j == i ? 1.0 : 0.0;
+        if (j <= i) Lp[tri(r0 + i, r0 + j)] = a[j];
+        LI[K * 256 + j * 16 + i] = e[j];
       }
-      bool ok = true;
-      unroll<16>([&](auto Kc) {
-        constexpr int k = Kc;
-        // pivot row k of the Schur complement = column k (symmetry): lane k's
-        // entries, broadcast by DPP
-        const double akk = bc<k>(a[k]);
-        ok = ok && (akk > 0.0);
-        const double ik = rsq1(akk);  // hardware estimate + one Newton step (qpb_common.h)
-        const double ik2 = ik * ik;
-        const double c = a[k] * ik2;
-        const double ne2 = -(e[k] * ik2);
-        e[k] *= ik;
-        unroll<15 - k>([&](auto J) {
-          constexpr int j = k + 1 + J;
-          const double pj = bc<k>(a[j]);
-          e[j] = __builtin_fma(ne2, pj, e[j]);
-          a[j] = __builtin_fma(-c, pj, a[j]);
-          // materialised inside the step: IR passes would otherwise sink the
-          // updates and keep every step's broadcasts alive (qpb_gi.hip)
-          pin(e[j]);
-          pin(a[j]);
-        });
-        a[k] *= ik;
-      });
-      if (l < 16) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (j <= i) Lp[tri(r0 + i, r0 + j)] = a[j];
-          LI[K * 256 + j * 16 + i] = e[j];
-        }
-      }
-      if (l == 0 && !ok) flags[0] = 1;
     }
-    __syncthreads();
+    if (l == 0 && !ok) flags[0] = 1;
+      };
+  const int li = l & 15, lk = l >> 4;
+  // one tile update (I, J) -= L[I, K] L[J, K]^T on the matrix cores (two
+  // tiles at a time: independent MFMA chains); `on` masks the second one
+  auto tile_update2 = [&](int K, const int (&I)[2], const int (&J)[2], const bool (&on)[2]) {
+    d4 acc[2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I[h2] + lk + 4 * r, col = 16 * J[h2] + li;
+        acc[h2][r] = row >= col ? Lp[tri(row, col)] : 0.0;
+      }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        mfma(-Lp[tri(16 * I[h2] + li, 16 * K + 4 * s + lk)], Lp[tri(16 * J[h2] + li, 16 * K + 4 * s + lk)], acc[h2]);
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I[h2] + lk + 4 * r, col = 16 * J[h2] + li;
+        if (on[h2] && row >= col) Lp[tri(row, col)] = acc[h2][r];
+      }
+  };
+  if (wv == 0) factor_diag(0);
+  __syncthreads();
+  for (int K = 0; K < T; ++K) {
     clk.tick(12);
     // panel: L[I, K] = H~[I, K] Linv_K^T, one tile per wavefront
-    const int li = l & 15, lk = l >> 4;
     if (wv < T - K - 1) {
       const int I = K + 1 + wv;
       d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -262,46 +290,41 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
     }
     __syncthreads();
     clk.tick(13);
-    // trailing tiles (I, J), K < J <= I < T, round robin over the wavefronts
-    const int nr = T - K - 1, ntile = nr * (nr + 1) / 2;
-    // two tiles per wavefront at a time: two independent MFMA chains
-    for (int t0 = wv; t0 < ntile; t0 += 2 * NWV) {
-      int I[2], J[2];
-      bool on[2];
+    if (K + 1 < T) {
+      // look-ahead: wavefront 0 updates the next diagonal tile and factorises
+      // it while the others update the rest of the trailing matrix
+      const int nr = T - K - 1, ntile = nr * (nr + 1) / 2 - 1;  // all but (K+1, K+1)
+      if (wv == 0) {
+        const int I[2] = {K + 1, K + 1}, J[2] = {K + 1, K + 1};
+        const bool on[2] = {true, false};
+        tile_update2(K, I, J, on);
+        wave_lds_sync();
+        factor_diag(K + 1);
+      } else if (wv != 4) {
+        // waves 1-3, 5-7: wave 4 shares wavefront 0's SIMD and stays idle, so
+        // the diagonal factorisation (the critical path) keeps its issue slots
+        const int wr = wv < 4 ? wv - 1 : wv - 2;
+        constexpr int NTW = NWV - 2;
+        for (int t0 = wr; t0 < ntile; t0 += 2 * NTW) {
+          int I[2], J[2];
+          bool on[2];
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int t = t0 + NWV * h2;
-        on[h2] = t < ntile;
-        const int tt = on[h2] ? t : t0;
-        int i = (int)((__builtin_sqrt(8.0 * tt + 1.0) - 1.0) * 0.5);
-        if (tri(i + 1, 0) <= tt) ++i;
-        if (tri(i, 0) > tt) --i;
-        J[h2] = tt - tri(i, 0) + K + 1;
-        I[h2] = i + K + 1;
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int t = t0 + NTW * h2;
+            on[h2] = t < ntile;
+            // tiles in row-major lower order after (K+1, K+1): index t + 1
+            const int tt = (on[h2] ? t : t0) + 1;
+            int i = (int)((__builtin_sqrt(8.0 * tt + 1.0) - 1.0) * 0.5);
+            if (tri(i + 1, 0) <= tt) ++i;
+            if (tri(i, 0) > tt) --i;
+            J[h2] = tt - tri(i, 0) + K + 1;
+            I[h2] = i + K + 1;
+          }
+          tile_update2(K, I, J, on);
+        }
       }
-      d4 acc[2];
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * I[h2] + lk + 4 * r, col = 16 * J[h2] + li;
-          acc[h2][r] = row >= col ? Lp[tri(row, col)] : 0.0;
-        }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2)
-          mfma(-Lp[tri(16 * I[h2] + li, 16 * K + 4 * s + lk)], Lp[tri(16 * J[h2] + li, 16 * K + 4 * s + lk)],
-               acc[h2]);
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * I[h2] + lk + 4 * r, col = 16 * J[h2] + li;
-          if (on[h2] && row >= col) Lp[tri(row, col)] = acc[h2][r];
-        }
+      __syncthreads();
     }
-    __syncthreads();
     clk.tick(14);
   }
   return flags[0] == 0;
@@ -495,6 +518,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     clk.tick(1);
     double bl[RT], invn[RT], thr[RT], s[RT];
     bool zero_bad = false, act[RT];
+    int slot[RT];  // the active-set slot of this lane's row, -1 if inactive
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       const double nn2 = group_sum(na2[t]);
@@ -503,6 +527,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       thr[t] = (rowok[t] && nn2 > 0.0) ? -feas_tol * (1.0 + __builtin_fabs(bl[t]) * invn[t]) : -kInf;
       zero_bad = zero_bad || (rowok[t] && nn2 == 0.0 && bl[t] < -feas_tol * (1.0 + __builtin_fabs(bl[t])));
       act[t] = false;
+      slot[t] = -1;
     }
     if (tid == 0) flags[20] = 0;
     __syncthreads();
@@ -573,7 +598,10 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           }
       }
     };
-    if (tid < NB) iamb[tid] = -1;
+    if (tid < NB) {
+      iamb[tid] = -1;
+      lds[B_CB + tid] = 0.0;
+    }
     if (!done) publish_key();
     __syncthreads();
     while (!done && it < max_iter) {
@@ -594,7 +622,10 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         row_dot(E, ub + 34 * lk, vr);  // v = D u: column p of G
         if (lk == 0) {
 #pragma unroll
-          for (int t = 0; t < RT; ++t) vb[row[t]] = vr[t];
+          for (int t = 0; t < RT; ++t) {
+            vb[row[t]] = vr[t];
+            if (slot[t] >= 0) lds[B_CB + slot[t]] = vr[t];  // c = v[W], by slot
+          }
         }
         __syncthreads();
       }
@@ -605,18 +636,19 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       {
         const int t = 16 * wv + li;
         double acc0 = 0.0, acc1 = 0.0;
+        const double *cb = lds + B_CB;  // free slots: zero rows of G_WW^{-1}
         for (int i = lk; i < hi; i += 8) {
           const bool two = i + 4 < hi;
-          const int c0 = iamb[i], c2 = two ? iamb[i + 4] : -1;
           const double g0 = sym(Lp, t, i), g2 = two ? sym(Lp, t, i + 4) : 0.0;
-          acc0 = __builtin_fma(g0, c0 >= 0 ? vb[c0] : 0.0, acc0);
-          acc1 = __builtin_fma(g2, c2 >= 0 ? vb[c2] : 0.0, acc1);
+          acc0 = __builtin_fma(g0, cb[i], acc0);
+          acc1 = __builtin_fma(g2, two ? cb[i + 4] : 0.0, acc1);
         }
         const double rt = group_sum(acc0 + acc1);
         double ratio = kBig;
         if (t < hi) {
           if (lk == 0) rb[t] = rt;
-          if (rt > 0.0 && iamb[t] >= 0) ratio = lamb[t] * rcp(rt);
+          const bool occupied = ((t < 64 ? occ0 >> t : occ1 >> (t - 64)) & 1ull) != 0;
+          if (rt > 0.0 && occupied) ratio = lamb[t] * rcp(rt);
         }
         const double wmin = row_min(ratio);  // the wave's 16 slots (every row holds them)
         // first slot reaching the minimum
@@ -656,6 +688,9 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       }
       __syncthreads();
       clk.tick(5);
+      // ---- slack direction D w (issued before the scalar chain below needs it)
+      double ds[RT];
+      row_dot(E, wb + 34 * lk, ds);
       // ---- step lengths (identical arithmetic on every wavefront)
       double nd2 = 0.0;
 #pragma unroll
@@ -670,7 +705,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           t1 = red[R_T1 + 2 * w];
           kdrop = (int)red[R_T1 + 2 * w + 1];
         }
-      const double t2 = (nd2 > kDepTol * dd) ? -sp / nd2 : kBig;
+      const double t2 = (nd2 > kDepTol * dd) ? -sp * rcp(nd2) : kBig;
       const double tt = t1 < t2 ? t1 : t2;
       if (!(tt < kBig)) {
         status = QPB_INFEASIBLE;
@@ -678,8 +713,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       }
       clk.tick(15);
       if (t2 < kBig) {
-        double ds[RT];
-        row_dot(E, wb + 34 * lk, ds);  // slack direction D w
 #pragma unroll
         for (int t = 0; t < RT; ++t) s[t] = __builtin_fma(tt, ds[t], s[t]);
       }
@@ -691,15 +724,14 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         const int a = ~occ0 ? __builtin_ctzll(~occ0) : 64 + __builtin_ctzll(~occ1);
         const int hn = a + 1 > hi ? a + 1 : hi;
         const double inv = 1.0 / nd2;
-        for (int i = tid >> 3; i < hn; i += NT / 8) {
-          const double ri = rb[i];
-          for (int j = tid & 7; j <= i; j += 8) {
-            double &gij = Lp[tri(i, j)];
-            if (i == a) gij = j == a ? inv : -rb[j] * inv;
-            else if (j == a) gij = -ri * inv;
-            else if (i < hi) gij = __builtin_fma(ri * inv, rb[j], gij);
-          }
+        for (int i = tid >> 3; i < hi; i += NT / 8) {  // + r r^T / |w|^2 off slot a
+          const double ri = rb[i] * inv;
+          double *gi = Lp + tri(i, 0);
+          if (i != a)
+            for (int j = tid & 7; j <= i; j += 8)
+              if (j != a) gi[j] = __builtin_fma(ri, rb[j], gi[j]);
         }
+        if (tid < hn) Lp[tid >= a ? tri(tid, a) : tri(a, tid)] = tid == a ? inv : -rb[tid] * inv;
         if (tid == 0) {
           iamb[a] = p;
           lamb[a] = up;
@@ -709,7 +741,10 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         hi = hn;
 #pragma unroll
         for (int t = 0; t < RT; ++t)
-          if (row[t] == p) act[t] = true;
+          if (row[t] == p) {
+            act[t] = true;
+            slot[t] = a;
+          }
         selecting = true;
       } else {
         // ---- DROP slot k: Schur-complement downdate of G_WW^{-1} on the
@@ -718,7 +753,10 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         const int cdrop = iamb[k];
 #pragma unroll
         for (int t = 0; t < RT; ++t)
-          if (row[t] == cdrop) act[t] = false;
+          if (row[t] == cdrop) {
+            act[t] = false;
+            slot[t] = -1;
+          }
         const double ikk = 1.0 / Lp[tri(k, k)];
         for (int i = tid >> 3; i < hi; i += NT / 8) {
           if (i == k) continue;
