@@ -63,6 +63,9 @@
 #ifndef QPB_PF_DIST
 #define QPB_PF_DIST 0  // > 0: each wave prefetches the input lines of group blockIdx + QPB_PF_DIST
 #endif
+#ifndef QPB_XCH2
+#define QPB_XCH2 0  // 1: the owner lane writes both its D rows (no selects), s_p by a shuffle -- measured 5.7 % slower (profiles/r02/ab_xch.json)
+#endif
 #ifndef QPB_RATIO_MIN
 #define QPB_RATIO_MIN 1  // ratio test: exact f64 min + u32 argmin, no LDS round trip
 #endif
@@ -481,6 +484,26 @@ __device__ __forceinline__ void gi_group(
     // active columns are then zeroed in LDS: d2 = D[p, q:] (d = -D[p,:] in
     // G-I's sign convention; the signs are folded into the formulas below)
     const int owner = p & (NL - 1), prow = p >> 4;
+#if QPB_XCH2 && !QPB_DDINV
+    // both rows of the owner lane go out (16 stores instead of 34 selects +
+    // 8 stores); readers index row prow.  s_p arrives by a row shuffle.
+    double *xr = xch + (MR > 1 ? NL * prow : 0);
+    if (l == owner) {
+#pragma unroll
+      for (int r = 0; r < MR; ++r)
+#pragma unroll
+        for (int j = 0; j < NL; j += 2)
+          *reinterpret_cast<double2 *>(&xch[NL * r + j]) = make_double2(E[r][j], E[r][j + 1]);
+    }
+    double ssel = s[0];
+#pragma unroll
+    for (int r = 1; r < MR; ++r) ssel = prow == r ? s[r] : ssel;
+    const double sp = __shfl(ssel, owner, NL);
+    wave_lds_sync();
+    const double Dpl = xr[l];
+    const double Dpq = xr[q < NL ? q : 0];  // q == 16: only used by an ADD, impossible then
+#else
+    double *xr = xch;
     if (l == owner) {
 #pragma unroll
       for (int r = 0; r < MR; ++r)
@@ -503,12 +526,13 @@ __device__ __forceinline__ void gi_group(
 #else
     const double sp = xch[NL];
 #endif
+#endif
 
     wave_lds_sync();
-    if (l < q) xch[l] = 0.0;
+    if (l < q) xr[l] = 0.0;
     wave_lds_sync();
     double d2[NL];
-    lds_row16(xch, d2);
+    lds_row16(xr, d2);
     const double dl = -Dpl;  // d1 component of active position l
     const double nd2 = row_sum(l >= q ? Dpl * Dpl : 0.0);  // |d2|^2
 #if !QPB_DDINV
@@ -586,10 +610,10 @@ __device__ __forceinline__ void gi_group(
       const double nrm = nd2 * ir;
       const double alpha = Dpq <= 0.0 ? -nrm : nrm;
       const double beta = ir * rcp1(nrm + __builtin_fabs(Dpq));
-      if (l == q) xch[q] = Dpq + alpha;
+      if (l == q) xr[q] = Dpq + alpha;
       wave_lds_sync();
       double v[NL];
-      lds_row16(xch, v);
+      lds_row16(xr, v);
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const double w = beta * dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return v[j]; });
