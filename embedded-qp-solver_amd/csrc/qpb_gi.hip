@@ -66,6 +66,18 @@
 #ifndef QPB_XCH2
 #define QPB_XCH2 0  // 1: the owner lane writes both its D rows (no selects), s_p by a shuffle -- measured 5.7 % slower (profiles/r02/ab_xch.json)
 #endif
+#ifndef QPB_RPRE
+#define QPB_RPRE 0  // back substitution: row l of R read before the chain
+#endif
+#ifndef QPB_D2LATE
+#define QPB_D2LATE 0  // d2 read from LDS after the back substitution (shorter live range)
+#endif
+#ifndef QPB_HFUSE
+#define QPB_HFUSE 0  // ADD: Householder products from the slack step's D d2 plus alpha D[:, q]
+#endif
+#ifndef QPB_XCHM
+#define QPB_XCHM 0  // exchange: one exec-masked store block per D row (no row selects)
+#endif
 #ifndef QPB_RATIO_MIN
 #define QPB_RATIO_MIN 1  // ratio test: exact f64 min + u32 argmin, no LDS round trip
 #endif
@@ -504,7 +516,26 @@ __device__ __forceinline__ void gi_group(
     const double Dpq = xr[q < NL ? q : 0];  // q == 16: only used by an ADD, impossible then
 #else
     double *xr = xch;
+#if QPB_XCHM && !QPB_DDINV
+    // one masked block per row: distinct asm markers keep the compiler from
+    // merging the blocks' stores into selects + one store block
+    if (l == owner && prow == 0) {
+      asm volatile("; xchm row 0" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[0][j], E[0][j + 1]);
+      xch[NL] = s[0];
+    }
+    if (MR > 1 && l == owner && prow == 1) {
+      asm volatile("; xchm row 1" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < NL; j += 2)
+        *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[MR - 1][j], E[MR - 1][j + 1]);
+      xch[NL] = s[MR - 1];
+    }
+    if (false) {
+#else
     if (l == owner) {
+#endif
 #pragma unroll
       for (int r = 0; r < MR; ++r)
         if (r == prow) {
@@ -532,7 +563,9 @@ __device__ __forceinline__ void gi_group(
     if (l < q) xr[l] = 0.0;
     wave_lds_sync();
     double d2[NL];
+#if !QPB_D2LATE
     lds_row16(xr, d2);
+#endif
     const double dl = -Dpl;  // d1 component of active position l
     const double nd2 = row_sum(l >= q ? Dpl * Dpl : 0.0);  // |d2|^2
 #if !QPB_DDINV
@@ -543,7 +576,21 @@ __device__ __forceinline__ void gi_group(
     // ---- r = R^{-1} d1: lane-parallel back substitution over the active positions
     double rm = 0.0;
     if (qmax > 0) {
-#if QPB_DPPFMA
+#if QPB_RPRE
+      // row l of R read up front (independent of the substitution chain), so
+      // the chain waits for LDS once instead of once per step
+      double rrow[NL];
+      unroll<8>([&](auto J) { rrow[J] = R[J * NL + l]; });
+      if (qmax > 8) unroll<8>([&](auto J) { rrow[8 + J] = R[(8 + J) * NL + l]; });
+      else unroll<8>([&](auto J) { rrow[8 + J] = 0.0; });
+      const double ninv = -invRd;
+      double nacc = (l < q) ? Dpl : 0.0;  // = -d1_l
+      unroll<NL>([&](auto JJ) {
+        constexpr int j = NL - 1 - JJ;
+        if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, rrow[j]);
+      });
+      rm = nacc * ninv;
+#elif QPB_DPPFMA
       // on the negated accumulator: nacc_l += R[l][j] * r_j, r_j = nacc_j * (-1/R_jj)
       // read from lane j by the FMA itself (the product was written just
       // before: fmac_bc_nop issues the DPP read hazard's wait states)
@@ -591,10 +638,21 @@ __device__ __forceinline__ void gi_group(
       done = true;
       break;
     }
+#if QPB_HFUSE
+    double ed2[MR];  // D[r, :] d2, reused by an ADD's reflection
+#endif
     if (t2 < kBig) {  // primal step: slacks s -= t A z,  A z = -D[:, q:] d2
+#if QPB_D2LATE
+      lds_row16(xr, d2);
+#endif
 #pragma unroll
-      for (int r = 0; r < MR; ++r)
-        s[r] = __builtin_fma(t, dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return d2[j]; }), s[r]);
+      for (int r = 0; r < MR; ++r) {
+        const double u = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return d2[j]; });
+#if QPB_HFUSE
+        ed2[r] = u;
+#endif
+        s[r] = __builtin_fma(t, u, s[r]);
+      }
     }
 #pragma unroll
     for (int r = 0; r < MR; ++r) pin(s[r]);  // d2 dies here, before the ADD reads v
@@ -614,9 +672,30 @@ __device__ __forceinline__ void gi_group(
       wave_lds_sync();
       double v[NL];
       lds_row16(xr, v);
+#if QPB_HFUSE
+      // D v = D d2 + alpha D[:, q]: column q picked by a select chain over the
+      // wave's range of q (usually one or two values) instead of a second
+      // 16-term product per row
+      double eq[MR];
+#pragma unroll
+      for (int r = 0; r < MR; ++r) eq[r] = 0.0;
+      const int qlo = wave_min4(q);
+      unroll<NL>([&](auto J) {
+        constexpr int j = J;
+        if (j >= qlo && j <= qmax) {
+          const bool hit = q == j;
+#pragma unroll
+          for (int r = 0; r < MR; ++r) eq[r] = hit ? E[r][j] : eq[r];
+        }
+      });
+#endif
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
+#if QPB_HFUSE
+        const double w = beta * __builtin_fma(alpha, eq[r], ed2[r]);
+#else
         const double w = beta * dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return v[j]; });
+#endif
 #pragma unroll
         for (int j = 0; j < NL; ++j) E[r][j] = __builtin_fma(-w, v[j], E[r][j]);
       }
@@ -864,8 +943,11 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
                          lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags);
     } else if (n16 && d->m == 32 && (d->flags & 4))  // diagnostic: the 2-waves/SIMD build
       QPB_GI_LAUNCH(2, true, true);
+#ifndef QPB_GI_XLDS
+#define QPB_GI_XLDS 0  // diagnostic: extra dynamic LDS per wave (lowers occupancy)
+#endif
     else if (n16 && d->m == 32)  // 168 VGPRs, 13.25 KiB LDS: 3 waves per SIMD
-      hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream,
+      hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true, false, 3>), dim3((unsigned)blocks), dim3(64), QPB_GI_XLDS, stream,
                          H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
                          d->flags);
     else if (n16) QPB_GI_LAUNCH(2, true, false);

@@ -42,6 +42,12 @@
 #include "qpb_common.h"
 #include "qpb.h"
 
+#ifndef GRAM_UNR
+#define GRAM_UNR 1  // unroll factor of the O(q) slot loops (LDS reads of several trips in flight)
+#endif
+#define GRAM_PRAGMA_(x) _Pragma(#x)
+#define GRAM_PRAGMA(x) GRAM_PRAGMA_(x)
+
 namespace qpb {
 namespace gram {
 
@@ -637,6 +643,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         const int t = 16 * wv + li;
         double acc0 = 0.0, acc1 = 0.0;
         const double *cb = lds + B_CB;  // free slots: zero rows of G_WW^{-1}
+        GRAM_PRAGMA(unroll GRAM_UNR)
         for (int i = lk; i < hi; i += 8) {
           const bool two = i + 4 < hi;
           const double g0 = sym(Lp, t, i), g2 = two ? sym(Lp, t, i + 4) : 0.0;
@@ -667,6 +674,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         double acc0 = 0.0, acc1 = 0.0;
         const int ha = hi < QL ? hi : QL;
         int j = lk;
+        GRAM_PRAGMA(unroll GRAM_UNR)
         for (; j + 4 < ha; j += 8) {
           acc0 = __builtin_fma(-rb[j], DW.lds[j * NB + c], acc0);
           acc1 = __builtin_fma(-rb[j + 4], DW.lds[(j + 4) * NB + c], acc1);

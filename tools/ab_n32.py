@@ -3,7 +3,7 @@
 rounds interleaved.  usage: python tools/ab_n32.py name[@flags] ...
 ('head' = lib/libqpb.so; flags = qpb_desc.flags, e.g. head@32 = mixed,
 head@96 = mixed without the fp64 re-solve).  env: B (262144), FAM (dense),
-ROUNDS (4), REPS (4)"""
+ROUNDS (4), REPS (4), N (32), M (64): any size class (e.g. N=128 M=256 B=16384 FAM=box)"""
 import ctypes
 import json
 import os
@@ -18,10 +18,11 @@ import qpb  # noqa: E402
 
 
 def main(names):
+    n, m = int(os.environ.get("N", 32)), int(os.environ.get("M", 64))
     B = int(os.environ.get("B", 262144))
     fam = os.environ.get("FAM", "dense")
     rounds, reps = int(os.environ.get("ROUNDS", 4)), int(os.environ.get("REPS", 4))
-    H, f, A, b = qpb.generate(32, B, 20261015, family=fam)
+    H, f, A, b = qpb.generate(n, B, 20261015, family=fam, m=m)
     libs, fl = {}, {}
     for nm in names:
         base, _, fs = nm.partition("@")
@@ -37,7 +38,7 @@ def main(names):
 
     def call(nm):
         o = sols[nm]
-        d = qpb.Desc(32, 64, B, 0, fl[nm], 0.0)
+        d = qpb.Desc(n, m, B, 0, fl[nm], 0.0)
         rc = libs[nm].qpb_solve(ctypes.byref(d), p(H), p(f), p(A), p(b), p(o.x), p(o.lam), p(o.active), p(o.status),
                                 p(o.iters), ctypes.c_void_p(s.cuda_stream))
         assert rc == 0, rc
