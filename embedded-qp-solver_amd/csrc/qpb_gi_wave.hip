@@ -19,6 +19,13 @@
 #include "qpb_common.h"
 #include "qpb.h"
 
+#ifndef WV_XFAST
+#define WV_XFAST 1  // outputs: active rows of A loaded all at once, L rows / columns prefetched, unrolled solves
+#endif
+#ifndef WV_KEY32
+#define WV_KEY32 1  // selection by 32-bit fp32-magnitude keys (DPP-fused v_max_u32, SALU across rows)
+#endif
+
 namespace qpb {
 namespace wv {
 
@@ -302,12 +309,27 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     if (selecting) {
       const double v = s * invn;
       const bool viol = !act && v < thr;
+#if WV_KEY32
+      // the fp32 magnitude of the (negative) normalised slack with the row in
+      // the low 6 bits (0 = none violated), as in qpb_gi.hip
+      uint32_t kk = viol ? ((__float_as_uint((float)(-v)) & ~63u) | (uint32_t)l) : 0u;
+      kk = row_max_u32(kk);
+      const uint32_t k0 = __builtin_amdgcn_readlane(kk, 0), k1 = __builtin_amdgcn_readlane(kk, 16);
+      const uint32_t k2 = __builtin_amdgcn_readlane(kk, 32), k3 = __builtin_amdgcn_readlane(kk, 48);
+      const uint32_t key = __builtin_elementwise_max(__builtin_elementwise_max(k0, k1), __builtin_elementwise_max(k2, k3));
+      if (key == 0u) {
+        status = QPB_OK;
+        break;
+      }
+      p = (int)(key & 63u);
+#else
       const double key = wave_min(viol ? pack_key64(v, l) : kBig);
       if (!(key < 0.0)) {
         status = QPB_OK;
         break;
       }
       p = __builtin_amdgcn_readfirstlane(key_index64(key));
+#endif
       up = 0.0;
       selecting = false;
     }
@@ -459,12 +481,73 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iact_k}, then L y = g,
   // L^T x = -y lane-parallel (L read from LDS, broadcasts by v_readlane)
   double gl = fl;
+  const int ll = l & (NP - 1);
+#if WV_XFAST
+  {
+    // every active row's element first (one memory round trip instead of q
+    // dependent ones), 8 at a time, then the sum
+    const int lc = l < n ? l : 0;
+    const int ias = iam > 0 ? iam : 0;
+    unroll<NP / 8>([&](auto Hh) {
+      constexpr int k0 = 8 * Hh;
+      if (k0 < q) {
+        double arow[8];
+        __builtin_amdgcn_sched_barrier(0);
+        unroll<8>([&](auto K) {
+          constexpr int kk = k0 + K;
+          arow[K] = kk < q ? Aq[__builtin_amdgcn_readlane(ias, kk) * n + lc] : 0.0;
+        });
+        unroll<8>([&](auto K) {
+          constexpr int kk = k0 + K;
+          if (kk < q) gl = __builtin_fma(readlane_d(um, kk), (l < n) ? arow[K] : 0.0, gl);
+        });
+      }
+    });
+  }
+  wave_lds_sync();
+  const double invd = ll < n ? rcp(Lp[lrow(ll) + ll]) : 0.0;
+  double acc = gl;
+  double yl = 0.0;
+  {
+    // row ll of L (entries past the diagonal read as zero), then the
+    // lane-parallel forward solve with constant-lane broadcasts
+    double Lrow[NP];
+    unroll<NP>([&](auto K) {
+      constexpr int kk = K;
+      Lrow[kk] = kk < ll ? Lp[lrow(ll) + kk] : 0.0;
+    });
+    unroll<NP>([&](auto K) {
+      constexpr int kk = K;
+      if (kk < n) {
+        const double yk = readlane_d(acc * invd, kk);
+        acc = __builtin_fma(-Lrow[kk], yk, acc);
+      }
+    });
+    yl = acc * invd;
+  }
+  acc = yl;
+  double xl;
+  {
+    double Lcol[NP];  // column ll of L below the diagonal
+    unroll<NP>([&](auto K) {
+      constexpr int kk = K;
+      Lcol[kk] = (kk > ll && kk < n) ? Lp[lrow(kk) + ll] : 0.0;
+    });
+    unroll<NP>([&](auto K) {
+      constexpr int kk = NP - 1 - K;
+      if (kk < n) {
+        const double xk = readlane_d(acc * invd, kk);
+        acc = __builtin_fma(-Lcol[kk], xk, acc);
+      }
+    });
+    xl = -(acc * invd);
+  }
+#else
   for (int kk = 0; kk < q; ++kk) {
     const int row = __builtin_amdgcn_readlane(iam, kk);
     const double u = readlane_d(um, kk);
     gl = __builtin_fma(u, (l < n) ? Aq[row * n + (l < n ? l : 0)] : 0.0, gl);
   }
-  const int ll = l & (NP - 1);
   wave_lds_sync();
   const double invd = ll < n ? rcp(Lp[lrow(ll) + ll]) : 0.0;
   double acc = gl;
@@ -482,6 +565,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     acc = __builtin_fma(-((ll < kk) ? Lp[lrow(kk) + ll] : 0.0), xk, acc);
   }
   xl = -xl;
+#endif
   if (status == QPB_OK && wave_any(l < n && !(__builtin_fabs(xl) < kInf))) status = QPB_NUMERICAL;
   clk.tick(10);  // x = -H^{-1} (f + A^T lam)
   // lambda scatter through LDS (64 entries over xch + the start of R)
@@ -515,9 +599,11 @@ extern "C" hipError_t qpb_launch_gi_wave(const qpb_desc *d, const double *H, con
                                          int32_t *iters, hipStream_t stream) {
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
-  // two waves per SIMD: at three the 168-VGPR cap spills the sweep (measured
-  // slower, profiles/r01/configs_v2.json)
-  hipLaunchKernelGGL(qpb::wv::gi_wave_kernel<2>, dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b, x, lam,
+  // three waves per SIMD: the 168-VGPR cap spills ~50 dwords, nearly all in
+  // the setup sweep; measured 6.30 ms against 6.47 ms for two waves with the
+  // same code at B = 262,144 (profiles/r02/ab_n32.json; round 1 measured
+  // the opposite on its kernel)
+  hipLaunchKernelGGL(qpb::wv::gi_wave_kernel<3>, dim3((unsigned)d->batch), dim3(64), 0, stream, H, f, A, b, x, lam,
                      active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol);
   return hipGetLastError();
 }
