@@ -79,9 +79,27 @@ def pmc_traffic(n: int, m: int, B: int, family: str, library: str):
     c = t.get("config", {})
     if (c.get("n"), c.get("m"), c.get("batch_per_gpu"), c.get("family")) != (n, m, B, family):
         return None
-    if t.get("library") != library:  # measured on another kernel revision
+    rev = t.get("kernel_rev")
+    if not rev or rev not in library:  # measured on another revision of the hot kernel
         return None
-    return {"bytes": t["hbm_bytes_per_launch"], "source": t.get("source", path)}
+    return {"bytes": t["hbm_bytes_per_launch"], "source": t.get("source", path),
+            "valu_insts_per_wave": t.get("valu_insts_per_wave"), "valu_source": t.get("valu_source")}
+
+
+VALU_CYCLES = 4  # one wave64 VALU instruction on a 16-lane SIMD (fp64 FMA at the 78.6 TF/s vector rate)
+SIMDS, CLOCK_GHZ = 1024, 2.4  # MI355X: 256 CUs x 4 SIMDs, peak engine clock
+
+
+def valu_ceiling(traffic, waves: int, kern_ms: float):
+    """The kernel's issue-rate bound: the PMC-measured VALU instructions per
+    wave (SQ_INSTS_VALU / SQ_WAVES, committed with the traffic numbers) issued
+    back to back on every SIMD at the peak clock, against the measured time."""
+    if not traffic or not traffic.get("valu_insts_per_wave"):
+        return None
+    ms = traffic["valu_insts_per_wave"] * VALU_CYCLES * waves / SIMDS / (CLOCK_GHZ * 1e9) * 1e3
+    return {"valu_insts_per_wave": traffic["valu_insts_per_wave"], "cycles_per_inst": VALU_CYCLES,
+            "ceiling_ms": ms, "kernel_ms": kern_ms, "frac": ms / kern_ms, "source": traffic.get("valu_source"),
+            "note": "time if every SIMD issued one VALU instruction every 4 cycles at 2.4 GHz with no stall"}
 
 
 # --------------------------------------------------------------------------- CPU share
@@ -342,8 +360,9 @@ def main():
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel": ("qpb::gi_dense_kernel" if n <= 16 and m <= 32
                                     else "qpb::wv::gi_wave_kernel" if n <= 32 and m <= 64
-                                    else "qpb::blk::gi_block_kernel"), "bytes_per_qp": bpq,
+                                    else "qpb::gram::gi_gram_kernel"), "bytes_per_qp": bpq,
                          "bytes_per_launch": B * bpq, "kernel_ms": kern_ms},
+            "valu_ceiling": valu_ceiling(traffic, (B + 3) // 4 if n <= 16 and m <= 32 else B, kern_ms),
             "cpu_baseline": cpu,
             "like_for_like": like,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
