@@ -78,6 +78,9 @@
 #ifndef QPB_XCHM
 #define QPB_XCHM 0  // exchange: one exec-masked store block per D row (no row selects)
 #endif
+#ifndef QPB_PRIO
+#define QPB_PRIO 0  // 1: s_setprio 2 in the active-set loop; 2: s_setprio 2 in the setup sweep
+#endif
 #ifndef QPB_RATIO_MIN
 #define QPB_RATIO_MIN 1  // ratio test: exact f64 min + u32 argmin, no LDS round trip
 #endif
@@ -314,6 +317,7 @@ __device__ __forceinline__ void gi_group(
   }
   const double fl = (N16 || l < n) ? fv : 0.0;
   clk.tick(0);
+  if constexpr (QPB_PRIO == 2) __builtin_amdgcn_s_setprio(2);
 
   // ---- H = L L^T, D = A L^{-T}, y = L^{-1} f: one right-looking sweep.
   // Step k: pr = row k of the current Schur complement (lane k's Lr, DPP
@@ -449,6 +453,8 @@ __device__ __forceinline__ void gi_group(
   int it = 0;
   wave_lds_sync();
   clk.tick(3);
+  if constexpr (QPB_PRIO == 1) __builtin_amdgcn_s_setprio(2);
+  if constexpr (QPB_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   // prefetch of the next group's H and A lines (one dword per 128-B line);
   // the values are only consumed at the end, so the loads retire in the
   // shadow of this group's iterations
@@ -787,6 +793,7 @@ __device__ __forceinline__ void gi_group(
     wave_lds_sync();
   }
   clk.tick(10);
+  if constexpr (QPB_PRIO == 1) __builtin_amdgcn_s_setprio(0);
 
   // ------------------------------------------------------------- outputs
   // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iact_k} (the active rows of

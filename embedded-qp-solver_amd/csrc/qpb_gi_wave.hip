@@ -26,6 +26,13 @@
 #define WV_KEY32 1  // selection by 32-bit fp32-magnitude keys (DPP-fused v_max_u32, SALU across rows)
 #endif
 
+#ifndef WV_BSU
+#define WV_BSU 0  // back solve unrolled, R entries read 8 steps ahead of the chain
+#endif
+#ifndef WV_DROP2
+#define WV_DROP2 0  // DROP: Givens parameters through LDS, then one unrolled rotation pass over D
+#endif
+
 namespace qpb {
 namespace wv {
 
@@ -34,7 +41,12 @@ constexpr int L_SIZE = NP * (NP + 1) / 2;           // 528
 constexpr int OFF_L = 0;
 constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*NP + i
 constexpr int OFF_X = OFF_R + NP * NP;              // 1552: exchange row (NP) + s_p, |d|^2; pivots
+#if WV_DROP2
+constexpr int OFF_G = OFF_X + NP + 8;               // 1592: Givens cosines | sines (DROP)
+constexpr int SLOT = OFF_G + 2 * NP;                // 1656 doubles = 13,248 B (12 waves per CU)
+#else
 constexpr int SLOT = OFF_X + NP + 8;                // 1592 doubles = 12,736 B
+#endif
 constexpr double kDepTol = 1e-24;
 
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
@@ -359,10 +371,28 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     double rm = 0.0;
     if (q > 0) {
       double acc = (l < q) ? dl : 0.0;
+#if WV_BSU
+      const int lc = l & (NP - 1);
+      unroll<NP / 8>([&](auto CC) {
+        constexpr int c0 = NP - 8 - 8 * CC;  // chunk of positions c0 .. c0 + 7, descending
+        if (c0 < q) {
+          double rc[8];
+          unroll<8>([&](auto I) { rc[I] = R[(c0 + I) * NP + lc]; });
+          unroll<8>([&](auto I) {
+            constexpr int j = c0 + 7 - I;
+            if (j < q) {
+              const double rj = readlane_d(acc * invRd, j);
+              acc = __builtin_fma(-rc[7 - I], rj, acc);
+            }
+          });
+        }
+      });
+#else
       for (int j = q - 1; j >= 0; --j) {
         const double rj = readlane_d(acc * invRd, j);
         acc = __builtin_fma(-R[j * NP + (l & (NP - 1))], rj, acc);
       }
+#endif
       rm = acc * invRd;
     }
     clk.tick(5);  // back solve
@@ -450,6 +480,24 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
           R[l * NP + j] = __builtin_fma(cj, rj, sj * rj1);
           R[l * NP + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
         }
+#if WV_DROP2
+        lds[OFF_G + j] = cj;  // same value from every lane
+        lds[OFF_G + NP + j] = sj;
+      }
+      // the same rotations on columns j, j+1 of D, after the R sweep, in one
+      // unrolled pass with wave-uniform guards
+      wave_lds_sync();
+      unroll<NP - 1>([&](auto JJ) {
+        constexpr int jj = JJ;
+        if (jj >= k && jj < q - 1) {
+          const double cj = lds[OFF_G + jj], sj = lds[OFF_G + NP + jj];
+          const double e0 = E[jj], e1 = E[jj + 1];
+          E[jj] = __builtin_fma(cj, e0, sj * e1);
+          E[jj + 1] = __builtin_fma(-sj, e0, cj * e1);
+        }
+      });
+      {
+#else
         // the same rotation on columns j, j+1 of D (j wave-uniform)
         unroll<NP - 1>([&](auto JJ) {
           constexpr int jj = JJ;
@@ -462,6 +510,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
             asm volatile("; rot %0" ::"n"(jj));
           }
         });
+#endif
       }
       wave_lds_sync();
       if (l < NP) R[l * NP + q - 1] = 0.0;
