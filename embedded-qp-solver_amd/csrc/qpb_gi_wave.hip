@@ -26,6 +26,9 @@
 #define WV_KEY32 1  // selection by 32-bit fp32-magnitude keys (DPP-fused v_max_u32, SALU across rows)
 #endif
 
+#ifndef WV_HFUSE
+#define WV_HFUSE 0  // ADD: D v = D d2 (the slack step's product) + alpha D[:, q], q wave-uniform
+#endif
 #ifndef WV_BSU
 #define WV_BSU 0  // back solve unrolled, R entries read 8 steps ahead of the chain
 #endif
@@ -413,7 +416,15 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       break;
     }
     // d2 is streamed from the exchange row (broadcast reads), not held
+#if WV_HFUSE
+    double ed2 = 0.0;  // D[l, :] d2, reused by an ADD's reflection
+    if (t2 < kBig) {
+      ed2 = dot_xch(E, xch);
+      s = __builtin_fma(t, ed2, s);
+    }
+#else
     if (t2 < kBig) s = __builtin_fma(t, dot_xch(E, xch), s);
+#endif
     pin(s);
     um = __builtin_fma(-t, rm, um);
     up += t;
@@ -427,7 +438,18 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       wave_lds_sync();
       if (l == q) xch[q] = Dpq + alpha;
       wave_lds_sync();
+#if WV_HFUSE
+      // column q of D by a wave-uniform switch (one QP per wave), instead of a
+      // second 32-term product: D v = D d2 + alpha D[:, q]
+      double eq = 0.0;
+      unroll<NP>([&](auto J) {
+        constexpr int j = J;
+        if (j == q) eq = E[j];
+      });
+      const double w = beta * __builtin_fma(alpha, eq, ed2);
+#else
       const double w = beta * dot_xch(E, xch);
+#endif
 #pragma unroll
       for (int j = 0; j < NP; j += 2) {
         const double2 v = *reinterpret_cast<const double2 *>(&xch[j]);
