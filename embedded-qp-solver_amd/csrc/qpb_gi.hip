@@ -78,6 +78,9 @@
 #ifndef QPB_XCHM
 #define QPB_XCHM 0  // exchange: one exec-masked store block per D row (no row selects)
 #endif
+#ifndef QPB_RSHIFT
+#define QPB_RSHIFT 0  // DROP: whole-column R copy, all reads issued before the writes
+#endif
 #ifndef QPB_PRIO
 #define QPB_PRIO 0  // 1: s_setprio 2 in the active-set loop; 2: s_setprio 2 in the setup sweep
 #endif
@@ -744,6 +747,24 @@ __device__ __forceinline__ void gi_group(
       wave_lds_sync();
       if (l < q) R[l * NL + l] = rdg;
       const bool shift = l >= k && l < q - 1;
+#if QPB_RSHIFT
+      {
+        // column l + 1 (16 contiguous doubles; its rows past l + 1 are zero)
+        // read whole by every lane before any lane writes: one LDS latency
+        wave_lds_sync();
+        double2 col[NL / 2];
+#pragma unroll
+        for (int t = 0; t < NL / 2; ++t) col[t] = *reinterpret_cast<const double2 *>(&R[((l + 1) & (NL - 1)) * NL + 2 * t]);
+        wave_lds_sync();
+        if (shift) {
+#pragma unroll
+          for (int t = 0; t < NL / 2; ++t) *reinterpret_cast<double2 *>(&R[l * NL + 2 * t]) = col[t];
+        } else if (l == q - 1) {
+#pragma unroll
+          for (int t = 0; t < NL / 2; ++t) *reinterpret_cast<double2 *>(&R[l * NL + 2 * t]) = make_double2(0.0, 0.0);
+        }
+      }
+#else
       for (int i = 0; i < qmax; ++i) {
         wave_lds_sync();
         const double nxt = R[((l + 1) & (NL - 1)) * NL + i];
@@ -751,6 +772,7 @@ __device__ __forceinline__ void gi_group(
         if (shift) R[l * NL + i] = nxt;
         else if (l == q - 1) R[l * NL + i] = 0.0;
       }
+#endif
       // Givens rotations restore the upper-triangular R
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
