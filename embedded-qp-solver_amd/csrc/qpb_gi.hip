@@ -81,6 +81,9 @@
 #ifndef QPB_RSHIFT
 #define QPB_RSHIFT 0  // DROP: whole-column R copy, all reads issued before the writes
 #endif
+#ifndef QPB_SELTHR
+#define QPB_SELTHR 0  // an active row's violation threshold is -inf (no act test in the selection)
+#endif
 #ifndef QPB_PRIO
 #define QPB_PRIO 0  // 1: s_setprio 2 in the active-set loop; 2: s_setprio 2 in the setup sweep
 #endif
@@ -482,9 +485,15 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const double v = s[r] * invn[r];
+#if QPB_SELTHR
+        const bool viol = v < thr[r];  // -inf while the row is active
+        const uint32_t kr = (__float_as_uint((float)(-v)) & ~31u) | (uint32_t)(l + NL * r);
+        key = viol ? (r == 0 ? kr : __builtin_elementwise_max(kr, key)) : key;
+#else
         const bool viol = !act[r] && v < thr[r];
         const uint32_t kr = (__float_as_uint((float)(-v)) & ~31u) | (uint32_t)(l + NL * r);
         key = viol && kr > key ? kr : key;
+#endif
       }
       key = row_max_u32(key);
       if (key == 0u) {
@@ -719,7 +728,12 @@ __device__ __forceinline__ void gi_group(
       if (l == owner) {
 #pragma unroll
         for (int r = 0; r < MR; ++r)
-          if (r == prow) act[r] = true;
+          if (r == prow) {
+            act[r] = true;
+#if QPB_SELTHR
+            thr[r] = -kInf;
+#endif
+          }
       }
       ++q;
       selecting = true;
@@ -730,7 +744,12 @@ __device__ __forceinline__ void gi_group(
       if (l == (c & (NL - 1))) {
 #pragma unroll
         for (int r = 0; r < MR; ++r)
-          if (r == (c >> 4)) act[r] = false;
+          if (r == (c >> 4)) {
+            act[r] = false;
+#if QPB_SELTHR
+            thr[r] = -feas_tol * (1.0 + __builtin_fabs(bl[r]) * invn[r]);  // an active row has a nonzero norm
+#endif
+          }
       }
       const double un = __shfl(um, (l + 1) & (NL - 1), NL);
       const int in = __shfl(iam, (l + 1) & (NL - 1), NL);
