@@ -211,14 +211,6 @@ __device__ __forceinline__ int wave_max4(int v) {
   return ab > cd ? ab : cd;
 }
 
-// ... and the min
-__device__ __forceinline__ int wave_min4(int v) {
-  const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
-  const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
-  const int ab = a < b ? a : b, cd = c < d ? c : d;
-  return ab < cd ? ab : cd;
-}
-
 // Diagnostic builds only (STAMP = true, qpb_solve_sections): s_memrealtime stamps
 // (100 MHz) accumulate each wave's ticks per kernel section; the real kernels have none.
 constexpr int kSections = 20;

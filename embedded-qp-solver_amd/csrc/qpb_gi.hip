@@ -66,27 +66,6 @@
 #ifndef QPB_XCH2
 #define QPB_XCH2 0  // 1: the owner lane writes both its D rows (no selects), s_p by a shuffle -- measured 5.7 % slower (profiles/r02/ab_xch.json)
 #endif
-#ifndef QPB_RPRE
-#define QPB_RPRE 0  // back substitution: row l of R read before the chain
-#endif
-#ifndef QPB_D2LATE
-#define QPB_D2LATE 0  // d2 read from LDS after the back substitution (shorter live range)
-#endif
-#ifndef QPB_HFUSE
-#define QPB_HFUSE 0  // ADD: Householder products from the slack step's D d2 plus alpha D[:, q]
-#endif
-#ifndef QPB_XCHM
-#define QPB_XCHM 0  // exchange: one exec-masked store block per D row (no row selects)
-#endif
-#ifndef QPB_RSHIFT
-#define QPB_RSHIFT 0  // DROP: whole-column R copy, all reads issued before the writes
-#endif
-#ifndef QPB_SELTHR
-#define QPB_SELTHR 0  // an active row's violation threshold is -inf (no act test in the selection)
-#endif
-#ifndef QPB_PRIO
-#define QPB_PRIO 0  // 1: s_setprio 2 in the active-set loop; 2: s_setprio 2 in the setup sweep
-#endif
 #ifndef QPB_RATIO_MIN
 #define QPB_RATIO_MIN 1  // ratio test: exact f64 min + u32 argmin, no LDS round trip
 #endif
@@ -323,7 +302,6 @@ __device__ __forceinline__ void gi_group(
   }
   const double fl = (N16 || l < n) ? fv : 0.0;
   clk.tick(0);
-  if constexpr (QPB_PRIO == 2) __builtin_amdgcn_s_setprio(2);
 
   // ---- H = L L^T, D = A L^{-T}, y = L^{-1} f: one right-looking sweep.
   // Step k: pr = row k of the current Schur complement (lane k's Lr, DPP
@@ -459,8 +437,6 @@ __device__ __forceinline__ void gi_group(
   int it = 0;
   wave_lds_sync();
   clk.tick(3);
-  if constexpr (QPB_PRIO == 1) __builtin_amdgcn_s_setprio(2);
-  if constexpr (QPB_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   // prefetch of the next group's H and A lines (one dword per 128-B line);
   // the values are only consumed at the end, so the loads retire in the
   // shadow of this group's iterations
@@ -485,15 +461,9 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const double v = s[r] * invn[r];
-#if QPB_SELTHR
-        const bool viol = v < thr[r];  // -inf while the row is active
-        const uint32_t kr = (__float_as_uint((float)(-v)) & ~31u) | (uint32_t)(l + NL * r);
-        key = viol ? (r == 0 ? kr : __builtin_elementwise_max(kr, key)) : key;
-#else
         const bool viol = !act[r] && v < thr[r];
         const uint32_t kr = (__float_as_uint((float)(-v)) & ~31u) | (uint32_t)(l + NL * r);
         key = viol && kr > key ? kr : key;
-#endif
       }
       key = row_max_u32(key);
       if (key == 0u) {
@@ -534,26 +504,7 @@ __device__ __forceinline__ void gi_group(
     const double Dpq = xr[q < NL ? q : 0];  // q == 16: only used by an ADD, impossible then
 #else
     double *xr = xch;
-#if QPB_XCHM && !QPB_DDINV
-    // one masked block per row: distinct asm markers keep the compiler from
-    // merging the blocks' stores into selects + one store block
-    if (l == owner && prow == 0) {
-      asm volatile("; xchm row 0" ::: "memory");
-#pragma unroll
-      for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[0][j], E[0][j + 1]);
-      xch[NL] = s[0];
-    }
-    if (MR > 1 && l == owner && prow == 1) {
-      asm volatile("; xchm row 1" ::: "memory");
-#pragma unroll
-      for (int j = 0; j < NL; j += 2)
-        *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[MR - 1][j], E[MR - 1][j + 1]);
-      xch[NL] = s[MR - 1];
-    }
-    if (false) {
-#else
     if (l == owner) {
-#endif
 #pragma unroll
       for (int r = 0; r < MR; ++r)
         if (r == prow) {
@@ -581,9 +532,7 @@ __device__ __forceinline__ void gi_group(
     if (l < q) xr[l] = 0.0;
     wave_lds_sync();
     double d2[NL];
-#if !QPB_D2LATE
     lds_row16(xr, d2);
-#endif
     const double dl = -Dpl;  // d1 component of active position l
     const double nd2 = row_sum(l >= q ? Dpl * Dpl : 0.0);  // |d2|^2
 #if !QPB_DDINV
@@ -594,21 +543,7 @@ __device__ __forceinline__ void gi_group(
     // ---- r = R^{-1} d1: lane-parallel back substitution over the active positions
     double rm = 0.0;
     if (qmax > 0) {
-#if QPB_RPRE
-      // row l of R read up front (independent of the substitution chain), so
-      // the chain waits for LDS once instead of once per step
-      double rrow[NL];
-      unroll<8>([&](auto J) { rrow[J] = R[J * NL + l]; });
-      if (qmax > 8) unroll<8>([&](auto J) { rrow[8 + J] = R[(8 + J) * NL + l]; });
-      else unroll<8>([&](auto J) { rrow[8 + J] = 0.0; });
-      const double ninv = -invRd;
-      double nacc = (l < q) ? Dpl : 0.0;  // = -d1_l
-      unroll<NL>([&](auto JJ) {
-        constexpr int j = NL - 1 - JJ;
-        if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, rrow[j]);
-      });
-      rm = nacc * ninv;
-#elif QPB_DPPFMA
+#if QPB_DPPFMA
       // on the negated accumulator: nacc_l += R[l][j] * r_j, r_j = nacc_j * (-1/R_jj)
       // read from lane j by the FMA itself (the product was written just
       // before: fmac_bc_nop issues the DPP read hazard's wait states)
@@ -656,19 +591,10 @@ __device__ __forceinline__ void gi_group(
       done = true;
       break;
     }
-#if QPB_HFUSE
-    double ed2[MR];  // D[r, :] d2, reused by an ADD's reflection
-#endif
     if (t2 < kBig) {  // primal step: slacks s -= t A z,  A z = -D[:, q:] d2
-#if QPB_D2LATE
-      lds_row16(xr, d2);
-#endif
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const double u = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return d2[j]; });
-#if QPB_HFUSE
-        ed2[r] = u;
-#endif
         s[r] = __builtin_fma(t, u, s[r]);
       }
     }
@@ -690,30 +616,9 @@ __device__ __forceinline__ void gi_group(
       wave_lds_sync();
       double v[NL];
       lds_row16(xr, v);
-#if QPB_HFUSE
-      // D v = D d2 + alpha D[:, q]: column q picked by a select chain over the
-      // wave's range of q (usually one or two values) instead of a second
-      // 16-term product per row
-      double eq[MR];
-#pragma unroll
-      for (int r = 0; r < MR; ++r) eq[r] = 0.0;
-      const int qlo = wave_min4(q);
-      unroll<NL>([&](auto J) {
-        constexpr int j = J;
-        if (j >= qlo && j <= qmax) {
-          const bool hit = q == j;
-#pragma unroll
-          for (int r = 0; r < MR; ++r) eq[r] = hit ? E[r][j] : eq[r];
-        }
-      });
-#endif
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
-#if QPB_HFUSE
-        const double w = beta * __builtin_fma(alpha, eq[r], ed2[r]);
-#else
         const double w = beta * dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return v[j]; });
-#endif
 #pragma unroll
         for (int j = 0; j < NL; ++j) E[r][j] = __builtin_fma(-w, v[j], E[r][j]);
       }
@@ -728,12 +633,7 @@ __device__ __forceinline__ void gi_group(
       if (l == owner) {
 #pragma unroll
         for (int r = 0; r < MR; ++r)
-          if (r == prow) {
-            act[r] = true;
-#if QPB_SELTHR
-            thr[r] = -kInf;
-#endif
-          }
+          if (r == prow) act[r] = true;
       }
       ++q;
       selecting = true;
@@ -744,12 +644,7 @@ __device__ __forceinline__ void gi_group(
       if (l == (c & (NL - 1))) {
 #pragma unroll
         for (int r = 0; r < MR; ++r)
-          if (r == (c >> 4)) {
-            act[r] = false;
-#if QPB_SELTHR
-            thr[r] = -feas_tol * (1.0 + __builtin_fabs(bl[r]) * invn[r]);  // an active row has a nonzero norm
-#endif
-          }
+          if (r == (c >> 4)) act[r] = false;
       }
       const double un = __shfl(um, (l + 1) & (NL - 1), NL);
       const int in = __shfl(iam, (l + 1) & (NL - 1), NL);
@@ -766,24 +661,6 @@ __device__ __forceinline__ void gi_group(
       wave_lds_sync();
       if (l < q) R[l * NL + l] = rdg;
       const bool shift = l >= k && l < q - 1;
-#if QPB_RSHIFT
-      {
-        // column l + 1 (16 contiguous doubles; its rows past l + 1 are zero)
-        // read whole by every lane before any lane writes: one LDS latency
-        wave_lds_sync();
-        double2 col[NL / 2];
-#pragma unroll
-        for (int t = 0; t < NL / 2; ++t) col[t] = *reinterpret_cast<const double2 *>(&R[((l + 1) & (NL - 1)) * NL + 2 * t]);
-        wave_lds_sync();
-        if (shift) {
-#pragma unroll
-          for (int t = 0; t < NL / 2; ++t) *reinterpret_cast<double2 *>(&R[l * NL + 2 * t]) = col[t];
-        } else if (l == q - 1) {
-#pragma unroll
-          for (int t = 0; t < NL / 2; ++t) *reinterpret_cast<double2 *>(&R[l * NL + 2 * t]) = make_double2(0.0, 0.0);
-        }
-      }
-#else
       for (int i = 0; i < qmax; ++i) {
         wave_lds_sync();
         const double nxt = R[((l + 1) & (NL - 1)) * NL + i];
@@ -791,7 +668,6 @@ __device__ __forceinline__ void gi_group(
         if (shift) R[l * NL + i] = nxt;
         else if (l == q - 1) R[l * NL + i] = 0.0;
       }
-#endif
       // Givens rotations restore the upper-triangular R
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
@@ -834,7 +710,6 @@ __device__ __forceinline__ void gi_group(
     wave_lds_sync();
   }
   clk.tick(10);
-  if constexpr (QPB_PRIO == 1) __builtin_amdgcn_s_setprio(0);
 
   // ------------------------------------------------------------- outputs
   // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iact_k} (the active rows of
@@ -991,11 +866,8 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
                          lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags);
     } else if (n16 && d->m == 32 && (d->flags & 4))  // diagnostic: the 2-waves/SIMD build
       QPB_GI_LAUNCH(2, true, true);
-#ifndef QPB_GI_XLDS
-#define QPB_GI_XLDS 0  // diagnostic: extra dynamic LDS per wave (lowers occupancy)
-#endif
     else if (n16 && d->m == 32)  // 168 VGPRs, 13.25 KiB LDS: 3 waves per SIMD
-      hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true, false, 3>), dim3((unsigned)blocks), dim3(64), QPB_GI_XLDS, stream,
+      hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream,
                          H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
                          d->flags);
     else if (n16) QPB_GI_LAUNCH(2, true, false);

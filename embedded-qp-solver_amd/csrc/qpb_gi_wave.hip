@@ -19,22 +19,7 @@
 #include "qpb_common.h"
 #include "qpb.h"
 
-#ifndef WV_XFAST
-#define WV_XFAST 1  // outputs: active rows of A loaded all at once, L rows / columns prefetched, unrolled solves
-#endif
-#ifndef WV_KEY32
-#define WV_KEY32 1  // selection by 32-bit fp32-magnitude keys (DPP-fused v_max_u32, SALU across rows)
-#endif
 
-#ifndef WV_HFUSE
-#define WV_HFUSE 0  // ADD: D v = D d2 (the slack step's product) + alpha D[:, q], q wave-uniform
-#endif
-#ifndef WV_BSU
-#define WV_BSU 0  // back solve unrolled, R entries read 8 steps ahead of the chain
-#endif
-#ifndef WV_DROP2
-#define WV_DROP2 0  // DROP: Givens parameters through LDS, then one unrolled rotation pass over D
-#endif
 
 namespace qpb {
 namespace wv {
@@ -44,12 +29,7 @@ constexpr int L_SIZE = NP * (NP + 1) / 2;           // 528
 constexpr int OFF_L = 0;
 constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*NP + i
 constexpr int OFF_X = OFF_R + NP * NP;              // 1552: exchange row (NP) + s_p, |d|^2; pivots
-#if WV_DROP2
-constexpr int OFF_G = OFF_X + NP + 8;               // 1592: Givens cosines | sines (DROP)
-constexpr int SLOT = OFF_G + 2 * NP;                // 1656 doubles = 13,248 B (12 waves per CU)
-#else
 constexpr int SLOT = OFF_X + NP + 8;                // 1592 doubles = 12,736 B
-#endif
 constexpr double kDepTol = 1e-24;
 
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
@@ -324,7 +304,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     if (selecting) {
       const double v = s * invn;
       const bool viol = !act && v < thr;
-#if WV_KEY32
       // the fp32 magnitude of the (negative) normalised slack with the row in
       // the low 6 bits (0 = none violated), as in qpb_gi.hip
       uint32_t kk = viol ? ((__float_as_uint((float)(-v)) & ~63u) | (uint32_t)l) : 0u;
@@ -337,14 +316,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
         break;
       }
       p = (int)(key & 63u);
-#else
-      const double key = wave_min(viol ? pack_key64(v, l) : kBig);
-      if (!(key < 0.0)) {
-        status = QPB_OK;
-        break;
-      }
-      p = __builtin_amdgcn_readfirstlane(key_index64(key));
-#endif
       up = 0.0;
       selecting = false;
     }
@@ -374,28 +345,10 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     double rm = 0.0;
     if (q > 0) {
       double acc = (l < q) ? dl : 0.0;
-#if WV_BSU
-      const int lc = l & (NP - 1);
-      unroll<NP / 8>([&](auto CC) {
-        constexpr int c0 = NP - 8 - 8 * CC;  // chunk of positions c0 .. c0 + 7, descending
-        if (c0 < q) {
-          double rc[8];
-          unroll<8>([&](auto I) { rc[I] = R[(c0 + I) * NP + lc]; });
-          unroll<8>([&](auto I) {
-            constexpr int j = c0 + 7 - I;
-            if (j < q) {
-              const double rj = readlane_d(acc * invRd, j);
-              acc = __builtin_fma(-rc[7 - I], rj, acc);
-            }
-          });
-        }
-      });
-#else
       for (int j = q - 1; j >= 0; --j) {
         const double rj = readlane_d(acc * invRd, j);
         acc = __builtin_fma(-R[j * NP + (l & (NP - 1))], rj, acc);
       }
-#endif
       rm = acc * invRd;
     }
     clk.tick(5);  // back solve
@@ -416,15 +369,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       break;
     }
     // d2 is streamed from the exchange row (broadcast reads), not held
-#if WV_HFUSE
-    double ed2 = 0.0;  // D[l, :] d2, reused by an ADD's reflection
-    if (t2 < kBig) {
-      ed2 = dot_xch(E, xch);
-      s = __builtin_fma(t, ed2, s);
-    }
-#else
     if (t2 < kBig) s = __builtin_fma(t, dot_xch(E, xch), s);
-#endif
     pin(s);
     um = __builtin_fma(-t, rm, um);
     up += t;
@@ -438,18 +383,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       wave_lds_sync();
       if (l == q) xch[q] = Dpq + alpha;
       wave_lds_sync();
-#if WV_HFUSE
-      // column q of D by a wave-uniform switch (one QP per wave), instead of a
-      // second 32-term product: D v = D d2 + alpha D[:, q]
-      double eq = 0.0;
-      unroll<NP>([&](auto J) {
-        constexpr int j = J;
-        if (j == q) eq = E[j];
-      });
-      const double w = beta * __builtin_fma(alpha, eq, ed2);
-#else
       const double w = beta * dot_xch(E, xch);
-#endif
 #pragma unroll
       for (int j = 0; j < NP; j += 2) {
         const double2 v = *reinterpret_cast<const double2 *>(&xch[j]);
@@ -502,24 +436,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
           R[l * NP + j] = __builtin_fma(cj, rj, sj * rj1);
           R[l * NP + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
         }
-#if WV_DROP2
-        lds[OFF_G + j] = cj;  // same value from every lane
-        lds[OFF_G + NP + j] = sj;
-      }
-      // the same rotations on columns j, j+1 of D, after the R sweep, in one
-      // unrolled pass with wave-uniform guards
-      wave_lds_sync();
-      unroll<NP - 1>([&](auto JJ) {
-        constexpr int jj = JJ;
-        if (jj >= k && jj < q - 1) {
-          const double cj = lds[OFF_G + jj], sj = lds[OFF_G + NP + jj];
-          const double e0 = E[jj], e1 = E[jj + 1];
-          E[jj] = __builtin_fma(cj, e0, sj * e1);
-          E[jj + 1] = __builtin_fma(-sj, e0, cj * e1);
-        }
-      });
-      {
-#else
         // the same rotation on columns j, j+1 of D (j wave-uniform)
         unroll<NP - 1>([&](auto JJ) {
           constexpr int jj = JJ;
@@ -532,7 +448,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
             asm volatile("; rot %0" ::"n"(jj));
           }
         });
-#endif
       }
       wave_lds_sync();
       if (l < NP) R[l * NP + q - 1] = 0.0;
@@ -553,7 +468,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // L^T x = -y lane-parallel (L read from LDS, broadcasts by v_readlane)
   double gl = fl;
   const int ll = l & (NP - 1);
-#if WV_XFAST
   {
     // every active row's element first (one memory round trip instead of q
     // dependent ones), 8 at a time, then the sum
@@ -613,30 +527,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     });
     xl = -(acc * invd);
   }
-#else
-  for (int kk = 0; kk < q; ++kk) {
-    const int row = __builtin_amdgcn_readlane(iam, kk);
-    const double u = readlane_d(um, kk);
-    gl = __builtin_fma(u, (l < n) ? Aq[row * n + (l < n ? l : 0)] : 0.0, gl);
-  }
-  wave_lds_sync();
-  const double invd = ll < n ? rcp(Lp[lrow(ll) + ll]) : 0.0;
-  double acc = gl;
-  double yl = 0.0;
-  for (int kk = 0; kk < n; ++kk) {
-    const double yk = readlane_d(acc * invd, kk);
-    if (l == kk) yl = yk;
-    acc = __builtin_fma(-((ll > kk) ? Lp[lrow(ll) + kk] : 0.0), yk, acc);
-  }
-  acc = yl;
-  double xl = 0.0;
-  for (int kk = n - 1; kk >= 0; --kk) {
-    const double xk = readlane_d(acc * invd, kk);
-    if (l == kk) xl = xk;
-    acc = __builtin_fma(-((ll < kk) ? Lp[lrow(kk) + ll] : 0.0), xk, acc);
-  }
-  xl = -xl;
-#endif
   if (status == QPB_OK && wave_any(l < n && !(__builtin_fabs(xl) < kInf))) status = QPB_NUMERICAL;
   clk.tick(10);  // x = -H^{-1} (f + A^T lam)
   // lambda scatter through LDS (64 entries over xch + the start of R)
