@@ -28,7 +28,7 @@
 // explicit inverse (:487-630) by the Cholesky and the triangular solves, the
 // vector ops (:158-411) fused into the iteration.
 //
-// One QP per 1024-thread workgroup (16 wavefronts, four per SIMD), one
+// One QP per 512-thread workgroup (8 wavefronts, two per SIMD), one
 // workgroup per CU; the workgroups pull QP indices from an atomic queue, so
 // QPs with long iteration counts do not hold up a static partition.
 // Registers: wave w owns rows 16w..16w+15 of D as eight 16 x 16 tiles in the
@@ -41,12 +41,6 @@
 // (loop; rows past QL live in a per-workgroup global scratch), vectors.
 #include "qpb_common.h"
 #include "qpb.h"
-
-#ifndef GRAM_UNR
-#define GRAM_UNR 1  // unroll factor of the O(q) slot loops (LDS reads of several trips in flight)
-#endif
-#define GRAM_PRAGMA_(x) _Pragma(#x)
-#define GRAM_PRAGMA(x) GRAM_PRAGMA_(x)
 
 namespace qpb {
 namespace gram {
@@ -643,7 +637,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         const int t = 16 * wv + li;
         double acc0 = 0.0, acc1 = 0.0;
         const double *cb = lds + B_CB;  // free slots: zero rows of G_WW^{-1}
-        GRAM_PRAGMA(unroll GRAM_UNR)
         for (int i = lk; i < hi; i += 8) {
           const bool two = i + 4 < hi;
           const double g0 = sym(Lp, t, i), g2 = two ? sym(Lp, t, i + 4) : 0.0;
@@ -674,7 +667,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         double acc0 = 0.0, acc1 = 0.0;
         const int ha = hi < QL ? hi : QL;
         int j = lk;
-        GRAM_PRAGMA(unroll GRAM_UNR)
         for (; j + 4 < ha; j += 8) {
           acc0 = __builtin_fma(-rb[j], DW.lds[j * NB + c], acc0);
           acc1 = __builtin_fma(-rb[j + 4], DW.lds[(j + 4) * NB + c], acc1);
