@@ -31,11 +31,12 @@
 // One QP per 512-thread workgroup (8 wavefronts, two per SIMD), one
 // workgroup per CU; the workgroups pull QP indices from an atomic queue, so
 // QPs with long iteration counts do not hold up a static partition.
-// Registers: wave w owns rows 16w..16w+15 of D as eight 16 x 16 tiles in the
-// matrix cores' C/D layout, which is also their B-operand layout: lane
-// (g = l >> 4, j = l & 15) holds D[16w + j][16k + g + 4r] (tile k, element r),
-// i.e. row j, the 32 columns congruent to g mod 4.  A row dot product is
-// 32 FMAs and two cross-group butterfly steps.
+// Registers: wave w owns rows 32w..32w+31 of D as two 16-row tiles (t) of
+// eight 16 x 16 column tiles (k) in the matrix cores' C/D layout, which is
+// also their B-operand layout: lane (g = l >> 4, j = l & 15) holds
+// D[32w + 16t + j][16k + g + 4r] (element r), i.e. in each row tile row j,
+// the 32 columns congruent to g mod 4.  A row dot product is 32 FMAs and two
+// cross-group butterfly steps.
 // LDS (160 KiB): the packed lower triangle (L in setup and finish, G_WW^{-1}
 // in the loop), the diagonal-tile inverses (setup) / the active rows D_W
 // (loop; rows past QL live in a per-workgroup global scratch), vectors.
