@@ -1,0 +1,57 @@
+"""Host logic of bench.py (CPU, no GPU): the algorithmic bytes per QP behind
+the roofline, the BASELINE config naming, the committed PMC
+lookup (keyed by the hot kernel's revision inside the library version string)
+and the VALU issue-rate ceiling computed from it."""
+import importlib.util
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)  # module level imports only the stdlib
+    return mod
+
+
+def test_bytes_per_qp_metric_config(bench):
+    # n = 16, m = 32: H 2048 + f 128 + A 4096 + b 256 in, x 128 + lam 256 + mask 4 + status 4 out
+    assert bench.bytes_per_qp(16, 32) == 6920
+    assert bench.bytes_per_qp(32, 64) == 8 * (1024 + 32 + 2048 + 64) + 8 * 96 + 8 + 4
+    assert bench.bytes_per_qp(128, 256) == 8 * (16384 + 128 + 32768 + 256) + 8 * 384 + 32 + 4
+
+
+def test_baseline_config_names(bench):
+    assert "configs[2]" in bench.baseline_config(16, 1 << 20, 8)
+    assert "configs[1]" in bench.baseline_config(16, 65536, 1)
+    assert "configs[4]" in bench.baseline_config(32, 262144, 1)
+    assert "configs[3]" in bench.baseline_config(128, 16384, 1)
+    assert bench.baseline_config(16, 1000, 1) == "not a BASELINE config"
+
+
+def test_pmc_traffic_is_keyed_by_kernel_revision(bench):
+    t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    c = t["config"]
+    lib_ok = "qpb x.y (gfx950; " + t["kernel_rev"] + ": ...)"
+    got = bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], c["family"], lib_ok)
+    assert got is not None and got["bytes"] == t["hbm_bytes_per_launch"]
+    assert got["valu_insts_per_wave"] == t["valu_insts_per_wave"]
+    # another revision of the hot kernel, or another configuration: no number
+    assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], c["family"], "qpb (gi_dense v0)") is None
+    assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"] // 2, c["family"], lib_ok) is None
+    assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], "dense", lib_ok) is None
+
+
+def test_valu_ceiling(bench):
+    assert bench.valu_ceiling(None, 1, 1.0) is None
+    t = {"valu_insts_per_wave": 3000.0, "valu_source": "x"}
+    waves = 1 << 18  # 1 M QPs, four per wave
+    v = bench.valu_ceiling(t, waves, 2.0)
+    # 3000 instructions x 4 cycles x 256 waves per SIMD at 2.4 GHz
+    assert v["ceiling_ms"] == pytest.approx(3000 * 4 * 256 / 2.4e9 * 1e3)
+    assert v["frac"] == pytest.approx(v["ceiling_ms"] / 2.0)
