@@ -34,6 +34,9 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
                                          const double *b, double *x, double *lam, uint32_t *active,
                                          int32_t *status, int32_t *iters, unsigned long long *sections,
                                          hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
+                                        const double *ub, double *x, double *lam, uint32_t *active, int32_t *status,
+                                        int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q,
                                      const double *x0, double *x, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
@@ -136,6 +139,32 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
     else
       e = qpb_launch_gi_gram(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, nullptr, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
+  }
+  return 0;
+}
+
+extern "C" int qpb_solve_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
+                             const double *ub, double *x, double *lam, uint32_t *active, int32_t *status,
+                             int32_t *iters, void *stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (d->m != 2 * d->n) return fail(QPB_ERR_INVALID_ARG, "qpb_solve_box: m must be 2n (got n=%d m=%d)", d->n, d->m);
+  if (d->n > 16)
+    return fail(QPB_ERR_UNSUPPORTED, "qpb_solve_box: n=%d > 16 (pass A = [I; -I], b = [ub; -lb] to qpb_solve)", d->n);
+  if (d->batch == 0) return 0;
+  if (!H || !f || !x || !lam || !active || !status)
+    return fail(QPB_ERR_INVALID_ARG, "H, f, x, lam, active and status are required");
+  rc = check_device();
+  if (rc) return rc;
+  // four QPs per wavefront: at most 2^27 QPs per launch (2^32 work-items)
+  const long long n = d->n, w = (2 * n + 31) / 32, step = 1LL << 27;
+  for (long long k0 = 0; k0 < d->batch; k0 += step) {
+    qpb_desc c = *d;
+    c.batch = d->batch - k0 < step ? d->batch - k0 : step;
+    hipError_t e = qpb_launch_gi_box(&c, H + k0 * n * n, f + k0 * n, lb ? lb + k0 * n : lb, ub ? ub + k0 * n : ub,
+                                     x + k0 * n, lam + k0 * 2 * n, active + k0 * w, status + k0,
+                                     iters ? iters + k0 : iters, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "qpb_solve_box launch");
   }
   return 0;
 }

@@ -63,6 +63,8 @@ _lib.qpb_solve.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 10
 _lib.qpb_solve.restype = ctypes.c_int
 _lib.qpb_solve_host.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 9
 _lib.qpb_solve_host.restype = ctypes.c_int
+_lib.qpb_solve_box.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 10
+_lib.qpb_solve_box.restype = ctypes.c_int
 _lib.qpb_ref_solve.argtypes = [ctypes.POINTER(RefDesc)] + [_vp] * 6
 _lib.qpb_ref_solve.restype = ctypes.c_int
 _lib.qpb_ref_solve_host.argtypes = [ctypes.POINTER(RefDesc)] + [_vp] * 5
@@ -151,6 +153,40 @@ def solve(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0, out
                         _ptr(out.x), _ptr(out.lam), _ptr(out.active), _ptr(out.status), _ptr(out.iters),
                         _stream_ptr(stream))
     _check(rc, "qpb_solve")
+    return out
+
+
+def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, feas_tol: float = 0.0, out: Solution | None = None,
+              stream=None) -> Solution:
+    """Batched min 1/2 x^T H x + f^T x s.t. lb <= x <= ub on the GPU (qpb_solve_box,
+    n <= 16): the reference admm()'s box QP (qp_solvers.c:146-319), solved exactly.
+
+    H (B,n,n), f (B,n), lb / ub (B,n) CUDA float64 tensors or None (absent
+    bounds; +-inf entries likewise).  The Solution has m = 2n: lam[:, :n] and
+    active bits 0..n-1 belong to the upper bounds, lam[:, n:] and bits n..2n-1
+    to the lower bounds (the row order of A = [I; -I], b = [ub; -lb]).
+    """
+    import torch
+    if not (H.is_cuda and f.is_cuda):
+        raise ValueError("qpb.solve_box expects CUDA (HIP) tensors")
+    B, n = f.shape
+    for t in (H, f, lb, ub):
+        if t is not None and (t.dtype != torch.float64 or not t.is_contiguous()):
+            raise ValueError("inputs must be contiguous float64")
+    if H.shape != (B, n, n) or any(t is not None and t.shape != (B, n) for t in (lb, ub)):
+        raise ValueError("shape mismatch")
+    dev = f.device
+    m = 2 * n
+    if out is None:
+        out = Solution(torch.empty((B, n), dtype=torch.float64, device=dev),
+                       torch.empty((B, m), dtype=torch.float64, device=dev),
+                       torch.empty((B, 1), dtype=torch.int32, device=dev),
+                       torch.empty((B,), dtype=torch.int32, device=dev),
+                       torch.empty((B,), dtype=torch.int32, device=dev))
+    d = Desc(n, m, B, max_iter, 0, feas_tol)
+    rc = _lib.qpb_solve_box(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(lb), _ptr(ub), _ptr(out.x), _ptr(out.lam),
+                            _ptr(out.active), _ptr(out.status), _ptr(out.iters), _stream_ptr(stream))
+    _check(rc, "qpb_solve_box")
     return out
 
 

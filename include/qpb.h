@@ -126,6 +126,19 @@ int qpb_solve_host(const qpb_desc *desc, const double *H, const double *f,
 		   const double *A, const double *b, double *x, double *lam,
 		   uint32_t *active, int32_t *status, int32_t *iters);
 
+/* Box-constrained batched solve, lb <= x <= ub: the constraint class of the
+ * reference's admm() (qp_solvers.c:146-319, bounds config.h:29-30), solved
+ * exactly with A = [I; -I], b = [ub; -lb] kept implicit (qpb_gi_box.hip).
+ * Replaces admm()'s box QP the way qpb_solve replaces the dense path.
+ * desc->n <= 16 (QPB_ERR_UNSUPPORTED above; pass the dense A = [I; -I] to
+ * qpb_solve there); desc->m must be 2n.  lb, ub: B x n, either may be NULL,
+ * and +-inf entries are absent bounds.  lam: B x 2n (upper bounds' multipliers
+ * first, then the lower bounds'), active: B words in the same row order;
+ * x, status, iters as qpb_solve.  Device pointers; asynchronous on `stream`. */
+int qpb_solve_box(const qpb_desc *desc, const double *H, const double *f,
+		  const double *lb, const double *ub, double *x, double *lam,
+		  uint32_t *active, int32_t *status, int32_t *iters, void *stream);
+
 /* Reference-semantics solvers (qp_solvers.c replicas). */
 typedef enum qpb_ref_mode {
 	QPB_REF_NEWTON = 1, /* qp_solvers.c:103-144 (explicit LU inverse, Armijo quirk) */

@@ -84,6 +84,27 @@ def test_argument_errors_without_gpu():
         assert b"no HIP device" in lib.qpb_last_error()
 
 
+def test_box_argument_errors_without_gpu():
+    lib = ctypes.CDLL(LIB)
+    lib.qpb_last_error.restype = ctypes.c_char_p
+    vp = ctypes.c_void_p
+    lib.qpb_solve_box.argtypes = [ctypes.POINTER(Desc)] + [vp] * 10
+    d = Desc(16, 30, 4, 0, 0, 0.0)  # m must be 2n
+    assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == -1
+    d = Desc(20, 40, 4, 0, 0, 0.0)  # the box kernel covers n <= 16
+    assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == -2
+    assert b"qpb_solve" in lib.qpb_last_error()
+    d = Desc(16, 32, 0, 0, 0, 0.0)
+    assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == 0
+    import torch
+    if not torch.cuda.is_available():
+        d = Desc(16, 32, 4, 0, 0, 0.0)
+        buf = ctypes.create_string_buffer(64)
+        p = ctypes.cast(buf, vp)
+        # lb / ub may be NULL (absent bounds); no device -> QPB_ERR_NO_DEVICE
+        assert lib.qpb_solve_box(ctypes.byref(d), p, p, None, None, p, p, p, p, None, None) == -4
+
+
 def test_python_binding_imports():
     import qpb
     assert qpb.version().startswith("qpb")
