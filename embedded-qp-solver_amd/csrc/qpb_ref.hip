@@ -132,13 +132,22 @@ __device__ void ref_invert(RefShared &S, int n) {
 
 // f(x) = 1/2 x^T (P x) + q^T x + r (quadratic_form_eval, qp.c:9-27); xv in LDS;
 // uses S.t2 as the P x temporary; result broadcast in S.scal[slot].
-__device__ double ref_eval(RefShared &S, const double *q, const double *xv, int n, int slot) {
+// The two sequential dots run on threads 0 and 1 at once (each in the
+// reference's order), then thread 0 combines them as the reference does.
+// `extra` (>= 0): thread 2 also computes fx + C2 * (t0 . t1) into scal[extra]
+// (the Armijo right-hand side, independent of f(x)).
+__device__ double ref_eval(RefShared &S, const double *q, const double *xv, int n, int slot, int extra = -1,
+                           double fx = 0.0) {
   const int tid = threadIdx.x;
   if (tid < n) S.t2[tid] = row_dot(S.P, xv, tid, n);
   __syncthreads();
+  if (tid == 0) S.scal[4] = seq_dot(xv, S.t2, n);
+  else if (tid == 1) S.scal[5] = seq_dot(q, xv, n);
+  else if (tid == 2 && extra >= 0) S.scal[extra] = fx + 1e-4 * seq_dot(S.t0, S.t1, n);  // C2 (qp_solvers.c:9)
+  __syncthreads();
   if (tid == 0) {
-    double a = 0.5 * seq_dot(xv, S.t2, n);
-    a += seq_dot(q, xv, n);
+    double a = 0.5 * S.scal[4];
+    a += S.scal[5];
     a += 0.0;  // r = 0 in every reference call path (main.c:12)
     S.scal[slot] = a;
   }
@@ -159,7 +168,7 @@ __device__ void ref_grad(RefShared &S, const double *q, const double *xv, double
 // line_search + armijo (qp_solvers.c:21-63); d in S.d, x in S.x; returns alpha
 __device__ double ref_line_search(RefShared &S, const double *q, int n) {
   const int tid = threadIdx.x;
-  const double C1 = 0.9, C2 = 1e-4;
+  const double C1 = 0.9;  // C2 = 1e-4 (qp_solvers.c:9) is applied in ref_eval
   const double fx = ref_eval(S, q, S.x, n, 1);
   ref_grad(S, q, S.x, S.t0, n);  // grad_fx
   double alpha = 1.0;            // ALPHA0_* (:11-12)
@@ -174,9 +183,7 @@ __device__ double ref_line_search(RefShared &S, const double *q, int n) {
     __syncthreads();
     if (tid < n) S.g[tid] = (S.x[tid] + S.t1[tid]) + S.t1[tid];  // lhs_arg = xk + d_alpha, xk = x + d_alpha
     __syncthreads();
-    const double lhs = ref_eval(S, q, S.g, n, 2);
-    if (tid == 0) S.scal[3] = fx + C2 * seq_dot(S.t0, S.t1, n);
-    __syncthreads();
+    const double lhs = ref_eval(S, q, S.g, n, 2, 3, fx);  // and rhs = fx + C2 (grad . d_alpha) in scal[3]
     const double rhs = S.scal[3];
     if (lhs <= rhs) break;
     alpha *= C1;
@@ -283,13 +290,18 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
         S.d[tid] = ds;
       }
       __syncthreads();
+      // the five norms (each the reference's sequential sum) on five threads at once
+      if (tid < 5) {
+        const double *v = tid == 0 ? S.g : tid == 1 ? S.d : tid == 2 ? S.x : tid == 3 ? z : u;
+        S.scal[2 + tid] = seq_norm(v, n);
+      }
+      __syncthreads();
       if (tid == 0) {
-        const double r_norm = seq_norm(S.g, n);
-        const double s_norm = seq_norm(S.d, n);
-        const double norm_x = seq_norm(S.x, n), norm_z = seq_norm(z, n);
+        const double r_norm = S.scal[2], s_norm = S.scal[3];
+        const double norm_x = S.scal[4], norm_z = S.scal[5];
         const double norm_max = norm_x > norm_z ? norm_x : norm_z;
         const double eps_pri = sq * abstol + restol * norm_max;  // :233-241
-        const double norm_u = seq_norm(u, n);
+        const double norm_u = S.scal[6];
         const double eps_dual = sq * abstol + restol * rho * norm_u;  // :243-253
         S.scal[0] = (r_norm < eps_pri && s_norm < eps_dual) ? 1.0 : 0.0;
       }
