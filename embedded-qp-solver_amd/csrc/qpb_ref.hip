@@ -263,31 +263,41 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
     __syncthreads();
     ref_invert(S, n);  // R^{-1} in S.V (:292)
     const double sq = __builtin_sqrt((double)n);
+    // admm_update_x's right-hand side rho (z - u) - q (:146-159) is each
+    // thread's own entry, so it is formed at the end of the previous
+    // iteration, into the other half of a double buffer (t1 / t2: the current
+    // one is still being read by every thread's row product)
+    if (tid < n) {
+      double y1 = z[tid] - u[tid];
+      y1 = rho * y1;
+      y1 = y1 - q[tid];
+      S.t1[tid] = y1;
+    }
+    __syncthreads();
     for (; it < iterations; ++it) {
+      double *ycur = (it & 1) ? S.t2 : S.t1, *ynext = (it & 1) ? S.t1 : S.t2;
       if (tid < n) {
-        S.t0[tid] = z[tid];  // z_old
-        double y1 = z[tid] - u[tid];  // admm_update_x (:146-159)
-        y1 = rho * y1;
-        y1 = y1 - q[tid];
-        S.t1[tid] = y1;
-      }
-      __syncthreads();
-      if (tid < n) {
-        const double xv = row_dot(S.V, S.t1, tid, n);
+        const double zold = z[tid];
+        const double xv = row_dot(S.V, ycur, tid, n);
         S.x[tid] = xv;
         double xh = alpha * xv;  // admm_update_x_hat (:161-174)
-        const double tz = (1.0 - alpha) * z[tid];
+        const double tz = (1.0 - alpha) * zold;
         xh = xh + tz;
         double tt = xh + u[tid];  // admm_update_z (:176-190): max with lb, then min with ub
         tt = tt > box_min ? tt : box_min;
         const double zn = tt > box_max ? box_max : tt;
         z[tid] = zn;
         const double du = xh - zn;  // admm_update_u (:192-203)
-        u[tid] = u[tid] + du;
+        const double un = u[tid] + du;
+        u[tid] = un;
         S.g[tid] = xv - zn;  // for admm_r_norm
-        double ds = zn - S.t0[tid];
+        double ds = zn - zold;
         ds = -rho * ds;  // admm_s_norm (:219-231)
         S.d[tid] = ds;
+        double y1 = zn - un;  // the next iteration's admm_update_x right-hand side
+        y1 = rho * y1;
+        y1 = y1 - q[tid];
+        ynext[tid] = y1;
       }
       __syncthreads();
       // the five norms (each the reference's sequential sum) on five threads at once
@@ -296,17 +306,14 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
         S.scal[2 + tid] = seq_norm(v, n);
       }
       __syncthreads();
-      if (tid == 0) {
-        const double r_norm = S.scal[2], s_norm = S.scal[3];
-        const double norm_x = S.scal[4], norm_z = S.scal[5];
-        const double norm_max = norm_x > norm_z ? norm_x : norm_z;
-        const double eps_pri = sq * abstol + restol * norm_max;  // :233-241
-        const double norm_u = S.scal[6];
-        const double eps_dual = sq * abstol + restol * rho * norm_u;  // :243-253
-        S.scal[0] = (r_norm < eps_pri && s_norm < eps_dual) ? 1.0 : 0.0;
-      }
-      __syncthreads();
-      if (S.scal[0] != 0.0) {
+      // the stopping test, evaluated identically by every thread (:233-253)
+      const double r_norm = S.scal[2], s_norm = S.scal[3];
+      const double norm_x = S.scal[4], norm_z = S.scal[5];
+      const double norm_max = norm_x > norm_z ? norm_x : norm_z;
+      const double eps_pri = sq * abstol + restol * norm_max;
+      const double norm_u = S.scal[6];
+      const double eps_dual = sq * abstol + restol * rho * norm_u;
+      if (r_norm < eps_pri && s_norm < eps_dual) {
         ++it;
         break;
       }
