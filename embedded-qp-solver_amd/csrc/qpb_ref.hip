@@ -78,14 +78,14 @@ __device__ void ref_invert(RefShared &S, int n) {
         }
       }
       S.scal[0] = piv;
-      S.perm[REF_MAXN] = pidx;
+      S.perm[n] = pidx;  // slot past the permutation
     }
     __syncthreads();
     if (S.scal[0] == 0.0) {  // singular: the reference prints and returns (:511-515)
       singular = true;
       break;
     }
-    const int pidx = S.perm[REF_MAXN];
+    const int pidx = S.perm[n];
     if (tid == 0) {  // permutation_swap :434-447
       const int tmp = S.perm[pidx];
       S.perm[pidx] = S.perm[k];
@@ -207,15 +207,17 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
   S.W = S.M + nn2;
   S.V = S.W + nn2;
   S.x = S.V + nn2;
-  S.g = S.x + REF_MAXN;
-  S.d = S.g + REF_MAXN;
-  S.t0 = S.d + REF_MAXN;
-  S.t1 = S.t0 + REF_MAXN;
-  S.t2 = S.t1 + REF_MAXN;
-  double *q = S.t2 + REF_MAXN;
-  double *u = q + REF_MAXN;
-  double *z = u + REF_MAXN;
-  S.scal = z + REF_MAXN;
+  // n-vectors packed at stride n: the LDS per QP sets the occupancy
+  // (n = 16: 9.6 KB, 16 workgroups per CU)
+  S.g = S.x + n;
+  S.d = S.g + n;
+  S.t0 = S.d + n;
+  S.t1 = S.t0 + n;
+  S.t2 = S.t1 + n;
+  double *q = S.t2 + n;
+  double *u = q + n;
+  double *z = u + n;
+  S.scal = z + n;
   S.perm = reinterpret_cast<int *>(S.scal + 8);
   const double *Pq = Pg + g * (long long)nn2;
   for (int e = tid; e < nn2; e += blockDim.x) S.P[e] = Pq[e];
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(REF_THREADS) void ref_invert_kernel(int n, long lon
 extern "C" hipError_t qpb_launch_ref_invert(int n, long long batch, const double *P, double *Pinv,
                                             hipStream_t stream) {
   if (n > qpb::REF_MAXN) return hipErrorInvalidValue;
-  const size_t lds = sizeof(double) * (3 * (size_t)n * n + 8) + sizeof(int) * (qpb::REF_MAXN + 2);
+  const size_t lds = sizeof(double) * (3 * (size_t)n * n + 8) + sizeof(int) * ((size_t)n + 2);
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&qpb::ref_invert_kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -398,7 +400,7 @@ extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, con
                                      double *x, int32_t *iters, hipStream_t stream) {
   if (d->n > qpb::REF_MAXN) return hipErrorInvalidValue;
   const int n = d->n;
-  const size_t lds = sizeof(double) * (4 * (size_t)n * n + 10 * qpb::REF_MAXN + 8) + sizeof(int) * (qpb::REF_MAXN + 2);
+  const size_t lds = sizeof(double) * (4 * (size_t)n * n + 10 * (size_t)n + 8) + sizeof(int) * ((size_t)n + 2);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&qpb::ref_kernel),
