@@ -66,26 +66,23 @@ __device__ void ref_invert(RefShared &S, int n) {
   __syncthreads();
   bool singular = false;
   for (int k = 0; k + 1 < n; ++k) {  // matrix_lup_decompose :507
-    if (tid == 0) {                  // matrix_lup_pivot :449-470 (first strict max)
-      double piv = 0.0;
-      int pidx = 0;
-      for (int i = k; i < n; ++i) {
-        double v = S.M[i * n + k];
-        v = v < 0 ? -v : v;
-        if (v > piv) {
-          piv = v;
-          pidx = i;
-        }
-      }
-      S.scal[0] = piv;
-      S.perm[n] = pidx;  // slot past the permutation
+    // matrix_lup_pivot :449-470: the first row attaining the largest |M[i][k]|
+    // (a strict `>` scan from piv = 0), found by a wave-wide exact max and the
+    // lowest lane holding it (one workgroup = one wavefront)
+    double v = 0.0;
+    if (tid >= k && tid < n) {
+      v = S.M[tid * n + k];
+      v = v < 0 ? -v : v;
     }
-    __syncthreads();
-    if (S.scal[0] == 0.0) {  // singular: the reference prints and returns (:511-515)
+    double piv = v;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) piv = __builtin_fmax(piv, __shfl_xor(piv, off));
+    if (!(piv > 0.0)) {  // singular: the reference prints and returns (:511-515)
       singular = true;
       break;
     }
-    const int pidx = S.perm[n];
+    const unsigned long long hit = __ballot(tid >= k && tid < n && v == piv);
+    const int pidx = __builtin_ctzll(hit);
     if (tid == 0) {  // permutation_swap :434-447
       const int tmp = S.perm[pidx];
       S.perm[pidx] = S.perm[k];
