@@ -24,7 +24,11 @@
 namespace qpb {
 namespace wv {
 
+#ifndef WV_HALF
+#define WV_HALF 1
+#endif
 constexpr int NP = 32;                              // padded n
+constexpr int NH = NP / 2;                          // H / L row half held per lane
 constexpr int L_SIZE = NP * (NP + 1) / 2;           // 528
 constexpr int OFF_L = 0;
 constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*NP + i
@@ -119,7 +123,13 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // of stride NP + 2 doubles (16-byte aligned rows, conflict-free b128 row
   // reads) and read back one row per lane: A rows 0-31, A rows 32-63, then H
   // (each part at most 32 rows = 16 loads of 64 lanes).
+#if WV_HALF
+  // row r = l & 31 of H / L is split over the two wave halves: lane r holds
+  // columns 0-15, lane r + 32 columns 16-31 (no idle upper half, 32 VGPRs)
+  double Lr[NH], E[NP];
+#else
   double Lr[NP], E[NP];
+#endif
   const double bv = bq[rowok ? l : 0];
   const double fv = fg[g * n + (l < n ? l : 0)];
   {
@@ -163,7 +173,9 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       }
     };
 #pragma unroll
-    for (int j = 0; j < NP; ++j) Lr[j] = E[j] = 0.0;
+    for (int j = 0; j < NP; ++j) E[j] = 0.0;
+#pragma unroll
+    for (int j = 0; j < (int)(sizeof(Lr) / sizeof(double)); ++j) Lr[j] = 0.0;
     // columns >= n of the staging rows stay zero for all three parts
 #pragma unroll
     for (int i = 0; i < (NP * RST + 127) / 128; ++i)
@@ -184,7 +196,19 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     }
     stage(hv);
     wave_lds_sync();
+#if WV_HALF
+    if ((l & (NP - 1)) < n) {
+      const double *src = &lds[(l & (NP - 1)) * RST + (l >> 5) * NH];
+#pragma unroll
+      for (int j = 0; j < NH; j += 2) {
+        const double2 v = *reinterpret_cast<const double2 *>(&src[j]);
+        Lr[j] = v.x;
+        Lr[j + 1] = v.y;
+      }
+    }
+#else
     fetch_row(Lr, l & (NP - 1), l < n);
+#endif
     wave_lds_sync();
   }
 
@@ -201,6 +225,135 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   if (l < NP) R[l] = 0.0;  // y capture (components >= n stay zero)
   bool spd = true;
   double ya = fl;
+#if WV_HALF
+  // Split rows: lane (h, r) = (l >> 5, l & 31) holds S[r][16h .. 16h + 15] of
+  // the Schur complement.  Step k: every lane stores its entry kk = k % 16 at
+  // pv[32h + r], so column k (= pivot row k by symmetry) is pv[32 kh + .],
+  // kh = k / 16, and each lane also reads its own S[r][k] there.  The half
+  // owning column k scales it into L[r][k]; entries left of it are final L
+  // (zero coefficient ch on the lower half), entries right of it take the
+  // Schur update.  Pivot pairs stream from LDS in double-buffered groups as
+  // below; for k < 16 the lower and upper halves read their own pairs.
+  const bool hi = l >= NP;
+  const int r = l & (NP - 1);
+  double *pv = R + 2 * NP;  // R is free until the loop (R[0..31]: y capture)
+  auto stream = [&](const double *src, auto NPAIRc, auto &&apply, auto &&pin_pair) {
+    constexpr int NPAIR = decltype(NPAIRc)::value, GP = 4, NG = (NPAIR + GP - 1) / GP;
+    if constexpr (NPAIR > 0) {
+      double2 buf[2][GP];
+      auto fetch = [&](auto G) {
+        constexpr int g = G;
+        unroll<GP>([&](auto I) {
+          constexpr int pr = g * GP + I;
+          if constexpr (pr < NPAIR) buf[g & 1][I] = *reinterpret_cast<const double2 *>(&src[2 * pr]);
+        });
+      };
+      fetch(std::integral_constant<int, 0>{});
+      unroll<NG>([&](auto G) {
+        constexpr int g = G;
+        if constexpr (g + 1 < NG) fetch(std::integral_constant<int, g + 1>{});
+        unroll<GP>([&](auto I) {
+          constexpr int pr = g * GP + I;
+          if constexpr (pr < NPAIR) apply(std::integral_constant<int, pr>{}, buf[g & 1][I]);
+        });
+        unroll<GP>([&](auto I) {
+          constexpr int pr = g * GP + I;
+          if constexpr (pr < NPAIR) pin_pair(std::integral_constant<int, pr>{});
+        });
+      });
+    }
+  };
+  unroll<NP>([&](auto K) {
+    constexpr int k = K, kh = k / NH, kk = k % NH;
+    if (k >= n) return;  // wave-uniform: padded columns stay zero
+    __builtin_amdgcn_sched_barrier(0);
+    wave_lds_sync();
+    pv[l] = Lr[kk];
+    wave_lds_sync();
+    const double akk = pv[NP * kh + k];
+    const double srk = pv[NP * kh + r];  // S[r][k]
+    spd = spd && (akk > 0.0);
+    const double ik = rsq(akk);
+    const double ik2 = ik * ik;
+    const double c = srk * ik2;
+    const double ch = hi ? c : 0.0;
+    const double e = E[k];
+    const double e2 = e * ik2;
+    E[k] = e * ik;
+    constexpr int j0 = (k + 1) / 2 * 2;
+    if constexpr (kh == 0) {
+      // Lr: own half's pairs (per-lane addresses), all 16 entries
+      stream(pv + NH * (l >> 5), std::integral_constant<int, NH / 2>{},
+             [&](auto PR, double2 v) {
+               constexpr int pr = PR;
+               unroll<2>([&](auto T) {
+                 constexpr int jj = 2 * pr + T;
+                 const double vj = T == 0 ? v.x : v.y;
+                 if constexpr (jj < kk) Lr[jj] = __builtin_fma(-ch, vj, Lr[jj]);
+                 else if constexpr (jj == kk) Lr[jj] = hi ? __builtin_fma(-c, vj, Lr[jj]) : Lr[jj] * ik;
+                 else Lr[jj] = __builtin_fma(-c, vj, Lr[jj]);
+               });
+             },
+             [&](auto PR) {
+               constexpr int pr = PR;
+               pin(Lr[2 * pr]);
+               pin(Lr[2 * pr + 1]);
+             });
+      // D row: columns j > k
+      stream(pv + j0, std::integral_constant<int, (NP - j0) / 2>{},
+             [&](auto PR, double2 v) {
+               constexpr int j = j0 + 2 * PR;
+               if constexpr (j >= k + 1) E[j] = __builtin_fma(-e2, v.x, E[j]);
+               E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
+             },
+             [&](auto PR) {
+               constexpr int j = j0 + 2 * PR;
+               if constexpr (j >= k + 1) pin(E[j]);
+               pin(E[j + 1]);
+             });
+    } else {
+      Lr[kk] = hi ? Lr[kk] * ik : Lr[kk];
+      // one stream feeds the D row (columns j > k) and the upper half's
+      // entries j - 16 (the lower half's are final: ch = 0 there)
+      stream(pv + NP + j0, std::integral_constant<int, (NP - j0) / 2>{},
+             [&](auto PR, double2 v) {
+               constexpr int j = j0 + 2 * PR;
+               if constexpr (j >= k + 1) {
+                 E[j] = __builtin_fma(-e2, v.x, E[j]);
+                 Lr[j - NH] = __builtin_fma(-ch, v.x, Lr[j - NH]);
+               }
+               E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
+               Lr[j + 1 - NH] = __builtin_fma(-ch, v.y, Lr[j + 1 - NH]);
+             },
+             [&](auto PR) {
+               constexpr int j = j0 + 2 * PR;
+               if constexpr (j >= k + 1) {
+                 pin(E[j]);
+                 pin(Lr[j - NH]);
+               }
+               pin(E[j + 1]);
+               pin(Lr[j + 1 - NH]);
+             });
+    }
+    const double fk = readlane_d(ya, k);
+    ya = __builtin_fma(-c, fk, ya);
+    R[k] = fk * ik;  // y_k, same-address store from every lane
+  });
+  clk.tick(1);  // sweep
+  // L -> LDS, packed rows: the upper half first, then the lower half, each in
+  // descending column order.  A dead entry (column j > r) lands in a later row
+  // at a smaller column, whose owner writes it afterwards (in-order DS).
+  unroll<NH>([&](auto J) {
+    constexpr int jj = NH - 1 - J;
+    if (hi) Lp[lrow(r) + NH + jj <= L_SIZE - 1 ? lrow(r) + NH + jj : L_SIZE - 1] = Lr[jj];
+    wave_lds_sync();
+  });
+  unroll<NH>([&](auto J) {
+    constexpr int jj = NH - 1 - J;
+    if (!hi) Lp[lrow(r) + jj] = Lr[jj];
+    wave_lds_sync();
+  });
+#else
   unroll<NP>([&](auto K) {
     constexpr int k = K;
     if (k >= n) return;  // wave-uniform: padded columns stay zero
@@ -277,6 +430,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     if (l < NP) Lp[lrow(l) + j <= L_SIZE - 1 ? lrow(l) + j : L_SIZE - 1] = Lr[j];
     wave_lds_sync();
   });
+#endif
   // y replicated: s = b + D y, |D row|^2
   wave_lds_sync();
   double yv[NP];
