@@ -2,15 +2,20 @@
 //
 // Same method as qpb_gi.hip (dual active set of Goldfarb & Idnani on
 // D = A L^{-T}, see there), mapped one QP per 64-lane wavefront: lane l owns
-// row l of D (and of H / L while factorising), every per-QP scalar is
-// wave-uniform, so control flow never diverges and no QP waits for another.
-// Broadcasts from one lane use v_readlane (SGPR results) or LDS.
+// row l of D, every per-QP scalar is wave-uniform, so control flow never
+// diverges and no QP waits for another.  Broadcasts from one lane use
+// v_readlane (SGPR results) or LDS.
 //
 // Setup, one right-looking sweep as in qpb_gi.hip, except that the pivot row
 // is gathered by symmetry: row k of the Schur complement is its column k, and
-// element k of lane j's row is a compile-time register index -- every lane
+// element k of a lane's row is a compile-time register index -- every lane
 // stores it, all lanes read the vector back (one b64 store + b128 broadcast
-// reads per step, no lane-selected writes).
+// reads per step, no lane-selected writes).  Row r of H / L is split over the
+// two wave halves (lane r: columns 0-15, lane r + 32: columns 16-31), so the
+// upper half carries half the Schur update instead of idling, and the row
+// costs 32 VGPRs instead of 64 (the sweep's spills went from 104 to 25 dwords;
+// 6.30 -> 5.88 ms at B = 262,144 with bitwise the same output,
+// profiles/r02/s4/ab_n32_half_sweep.json).
 //
 // LDS per QP (one wave): L packed rows (n(n+1)/2), R column-major NP x NP with
 // zero diagonal, the pivot / exchange vector, the y / x capture.
@@ -24,9 +29,6 @@
 namespace qpb {
 namespace wv {
 
-#ifndef WV_HALF
-#define WV_HALF 1
-#endif
 constexpr int NP = 32;                              // padded n
 constexpr int NH = NP / 2;                          // H / L row half held per lane
 constexpr int L_SIZE = NP * (NP + 1) / 2;           // 528
@@ -122,14 +124,10 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // eight QPs in flight per CU, thrash the vector L1), staged in LDS as rows
   // of stride NP + 2 doubles (16-byte aligned rows, conflict-free b128 row
   // reads) and read back one row per lane: A rows 0-31, A rows 32-63, then H
-  // (each part at most 32 rows = 16 loads of 64 lanes).
-#if WV_HALF
-  // row r = l & 31 of H / L is split over the two wave halves: lane r holds
-  // columns 0-15, lane r + 32 columns 16-31 (no idle upper half, 32 VGPRs)
+  // (each part at most 32 rows = 16 loads of 64 lanes); H row r = l & 31 is
+  // read back as half a row per lane (lane r: columns 0-15, lane r + 32:
+  // columns 16-31, the sweep's split layout).
   double Lr[NH], E[NP];
-#else
-  double Lr[NP], E[NP];
-#endif
   const double bv = bq[rowok ? l : 0];
   const double fv = fg[g * n + (l < n ? l : 0)];
   {
@@ -175,7 +173,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
 #pragma unroll
     for (int j = 0; j < NP; ++j) E[j] = 0.0;
 #pragma unroll
-    for (int j = 0; j < (int)(sizeof(Lr) / sizeof(double)); ++j) Lr[j] = 0.0;
+    for (int j = 0; j < NH; ++j) Lr[j] = 0.0;
     // columns >= n of the staging rows stay zero for all three parts
 #pragma unroll
     for (int i = 0; i < (NP * RST + 127) / 128; ++i)
@@ -196,7 +194,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     }
     stage(hv);
     wave_lds_sync();
-#if WV_HALF
     if ((l & (NP - 1)) < n) {
       const double *src = &lds[(l & (NP - 1)) * RST + (l >> 5) * NH];
 #pragma unroll
@@ -206,9 +203,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
         Lr[j + 1] = v.y;
       }
     }
-#else
-    fetch_row(Lr, l & (NP - 1), l < n);
-#endif
     wave_lds_sync();
   }
 
@@ -225,7 +219,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   if (l < NP) R[l] = 0.0;  // y capture (components >= n stay zero)
   bool spd = true;
   double ya = fl;
-#if WV_HALF
   // Split rows: lane (h, r) = (l >> 5, l & 31) holds S[r][16h .. 16h + 15] of
   // the Schur complement.  Step k: every lane stores its entry kk = k % 16 at
   // pv[32h + r], so column k (= pivot row k by symmetry) is pv[32 kh + .],
@@ -353,84 +346,6 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     if (!hi) Lp[lrow(r) + jj] = Lr[jj];
     wave_lds_sync();
   });
-#else
-  unroll<NP>([&](auto K) {
-    constexpr int k = K;
-    if (k >= n) return;  // wave-uniform: padded columns stay zero
-    __builtin_amdgcn_sched_barrier(0);
-    wave_lds_sync();
-    if (l < NP) xch[l] = Lr[k];  // column k = pivot row k (lanes >= 32 hold no H row)
-    wave_lds_sync();
-    const double akk = xch[k];
-    spd = spd && (akk > 0.0);
-    const double ik = rsq(akk);
-    const double ik2 = ik * ik;
-    const double c = Lr[k] * ik2;
-    const double e = E[k];
-    const double e2 = e * ik2;
-    Lr[k] *= ik;
-    E[k] = e * ik;
-    // the pivot row is streamed from LDS in 16-byte pairs, each pair feeding
-    // both the Schur update of row l and the substitution of D's row l.
-    // pin() is a scheduling barrier, so the reads go in groups of GP pairs,
-    // double-buffered: group g+1 is in flight while group g is applied (one
-    // exposed LDS latency per step instead of one per pair)
-    constexpr int j0 = (k + 1) / 2 * 2, NPAIR = (NP - j0) / 2, GP = 4, NG = (NPAIR + GP - 1) / GP;
-    if constexpr (NPAIR > 0) {
-      double2 buf[2][GP];
-      auto fetch = [&](auto G) {
-        constexpr int g = G;
-        unroll<GP>([&](auto I) {
-          constexpr int pr = g * GP + I;
-          if constexpr (pr < NPAIR) buf[g & 1][I] = *reinterpret_cast<const double2 *>(&xch[j0 + 2 * pr]);
-        });
-      };
-      fetch(std::integral_constant<int, 0>{});
-      unroll<NG>([&](auto G) {
-        constexpr int g = G;
-        if constexpr (g + 1 < NG) fetch(std::integral_constant<int, g + 1>{});
-        unroll<GP>([&](auto I) {
-          constexpr int pr = g * GP + I;
-          if constexpr (pr < NPAIR) {
-            constexpr int j = j0 + 2 * pr;
-            const double2 v = buf[g & 1][I];
-            if constexpr (j >= k + 1) {
-              Lr[j] = __builtin_fma(-c, v.x, Lr[j]);
-              E[j] = __builtin_fma(-e2, v.x, E[j]);
-            }
-            Lr[j + 1] = __builtin_fma(-c, v.y, Lr[j + 1]);
-            E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
-          }
-        });
-        unroll<GP>([&](auto I) {
-          constexpr int pr = g * GP + I;
-          if constexpr (pr < NPAIR) {
-            constexpr int j = j0 + 2 * pr;
-            if constexpr (j >= k + 1) {
-              pin(Lr[j]);
-              pin(E[j]);
-            }
-            pin(Lr[j + 1]);
-            pin(E[j + 1]);
-          }
-        });
-      });
-    }
-    const double fk = readlane_d(ya, k);
-    ya = __builtin_fma(-c, fk, ya);
-    R[k] = fk * ik;  // y_k, same-address store from every lane (R is free until the loop)
-  });
-  clk.tick(1);  // sweep
-  // L -> LDS (lane l < 32 writes row l; dead entries j > l land in later rows
-  // first and are overwritten by their owners: descending j, in-order DS;
-  // row 31's dead tail would run past L into R: clamped onto its own last entry,
-  // which its owner writes afterwards)
-  unroll<NP>([&](auto J) {
-    constexpr int j = NP - 1 - J;
-    if (l < NP) Lp[lrow(l) + j <= L_SIZE - 1 ? lrow(l) + j : L_SIZE - 1] = Lr[j];
-    wave_lds_sync();
-  });
-#endif
   // y replicated: s = b + D y, |D row|^2
   wave_lds_sync();
   double yv[NP];
