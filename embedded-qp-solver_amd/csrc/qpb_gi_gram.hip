@@ -206,15 +206,19 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
   const int nb = 16 * T;
   {
     // rows wv, wv + 8, ... (lanes along the columns: coalesced); every load
-    // is issued before the first store, one HBM round trip per QP
+    // is issued before the first store, one memory round trip per QP.  The
+    // loads are unconditional (addresses clamped into the row, so no extra
+    // lines): a guarded load becomes a branch with its own wait.
     double h[NB / NWV][2];
 #pragma unroll
     for (int u = 0; u < NB / NWV; ++u) {
       const int r = wv + NWV * u;
+      const int rr = r < n ? r : n - 1;
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int c = l + 64 * h2;
-        h[u][h2] = (r < n && c <= r) ? Hq[r * n + c] : (r == c ? 1.0 : 0.0);
+        const double v = Hq[rr * n + (c <= rr ? c : rr)];
+        h[u][h2] = (r < n && c <= r) ? v : (r == c ? 1.0 : 0.0);
       }
     }
 #pragma unroll
@@ -490,7 +494,11 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     // L kept in the workgroup's scratch for the final solve (the triangle
     // holds G_WW^{-1} during the loop); the loads back come after several
     // barriers on the same CU
-    for (int e = tid; e < tri(nb, 0); e += NT) Lgl[e] = Lp[e];
+#pragma unroll
+    for (int u = 0; u < (LP + NT - 1) / NT; ++u) {
+      const int e = tid + NT * u;
+      if (e < tri(nb, 0)) Lgl[e] = Lp[e];
+    }
     clk.tick(0);
     // y = L^{-1} f on wavefront 0, into yb (permuted), before D is live
     if (wv == 0) {
@@ -499,26 +507,54 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       yb[pad(perm(l))] = a0;
       yb[pad(perm(l + 64))] = a1;
     }
+    // this lane's entries of A and b, all issued before the first use: one
+    // memory round trip.  Loads are unconditional (masked lanes read a
+    // clamped address): a guarded load becomes a branch with its own wait.
+    // A's entries land in the registers of D, which the blocked substitution
+    // overwrites in place.
+    double E[RT][8][4];
+    double bl[RT];
+    if (m > 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = 16 * k + lk + 4 * r;
+            const bool ok = rowok[t] && col < n;
+            const double v = Aq[ok ? row[t] * n + col : 0];
+            E[t][k][r] = ok ? v : 0.0;
+          }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const double v = bg[g * m + (rowok[t] ? row[t] : 0)];
+        bl[t] = rowok[t] ? v : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) E[t][k][r] = 0.0;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) bl[t] = 0.0;
+    }
 
     // D = A L^{-T} on the matrix cores: tile k of D^T (16 columns of D x 16
     // rows) = (A^T's tile - sum_{j<k} L[k, j] D^T[j]) times Linv_k; the two
     // row tiles of the wave share every L operand
-    double E[RT][8][4];
     double na2[RT] = {};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) E[t][k][r] = 0.0;
       if (k < T) {
         d4 C[RT];
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int col = 16 * k + lk + 4 * r;
-            C[t][r] = (rowok[t] && col < n) ? Aq[row[t] * n + col] : 0.0;
+            C[t][r] = E[t][k][r];
             na2[t] = __builtin_fma(C[t][r], C[t][r], na2[t]);
           }
 #pragma unroll
@@ -545,13 +581,12 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       }
     }
     clk.tick(1);
-    double bl[RT], invn[RT], thr[RT], s[RT];
+    double invn[RT], thr[RT], s[RT];
     bool zero_bad = false, act[RT];
     int slot[RT];  // the active-set slot of this lane's row, -1 if inactive
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       const double nn2 = group_sum(na2[t]);
-      bl[t] = rowok[t] ? bg[g * m + row[t]] : 0.0;
       invn[t] = nn2 > 0.0 ? rsq(nn2) : 0.0;
       thr[t] = (rowok[t] && nn2 > 0.0) ? -feas_tol * (1.0 + __builtin_fabs(bl[t]) * invn[t]) : -kInf;
       zero_bad = zero_bad || (rowok[t] && nn2 == 0.0 && bl[t] < -feas_tol * (1.0 + __builtin_fabs(bl[t])));
@@ -840,7 +875,22 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     bool finite = true;
     clk.tick(7);
     if (spd) {
-      for (int e = tid; e < tri(nb, 0); e += NT) Lp[e] = Lgl[e];
+      // loads issued in passes of 6 before their stores: three round trips,
+      // not one per element pass (more registers here spill elsewhere)
+      const int ne = tri(nb, 0);
+      for (int e0 = tid; e0 < ne; e0 += 6 * NT) {
+        double lv[6];
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          const int e = e0 + NT * u;
+          lv[u] = Lgl[e < ne ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          const int e = e0 + NT * u;
+          if (e < ne) Lp[e] = lv[u];
+        }
+      }
       __syncthreads();
       clk.tick(8);
       if (wv == 0) {
