@@ -726,16 +726,21 @@ __device__ __forceinline__ void gi_group(
     const int lc = l < n ? l : n - 1;
     unroll<2>([&](auto H) {
       constexpr int k0 = 8 * H;
-      double arow[8];
-      __builtin_amdgcn_sched_barrier(0);
-      unroll<8>([&](auto K) {
-        constexpr int kk = k0 + K;
-        if (kk < qm) arow[K] = Aq[bci<kk>(ias) * n + lc];
-      });
-      unroll<8>([&](auto K) {
-        constexpr int kk = k0 + K;
-        if (kk < qm) gl = __builtin_fma(bc<kk>(um), (N16 || l < n) ? arow[K] : 0.0, gl);
-      });
+      // one wave-uniform test per group of eight: a test per load made each
+      // load of the second group a branch with its own wait (eight serial
+      // round trips); positions past qm read a valid row and are not summed
+      if (k0 < qm) {
+        double arow[8];
+        __builtin_amdgcn_sched_barrier(0);
+        unroll<8>([&](auto K) {
+          constexpr int kk = k0 + K;
+          arow[K] = Aq[bci<kk>(ias) * n + lc];
+        });
+        unroll<8>([&](auto K) {
+          constexpr int kk = k0 + K;
+          if (kk < qm) gl = __builtin_fma(bc<kk>(um), (N16 || l < n) ? arow[K] : 0.0, gl);
+        });
+      }
     });
   }
   const double invd = rcp1(Lp[lrow(l) + l]);

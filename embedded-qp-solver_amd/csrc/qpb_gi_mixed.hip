@@ -677,9 +677,16 @@ __global__ __launch_bounds__(64, OCC) void gi_mixed_kernel(
       if (rowok && !act && nrm2 > 0.f && (double)(s * invn) < tau) {
         const double *ar = Aq + l * n;
         double an = 0.0;
+        // clamped loads, all issued before the sum (the empty asm consumes
+        // them): a guarded load per j became a branch with its own wait
+        // (NP serial round trips)
+        double av[NP];
 #pragma unroll
-        for (int j = 0; j < NP; ++j)
-          if (j < n) an = __builtin_fma(ar[j], ar[j], an);
+        for (int j = 0; j < NP; ++j) av[j] = ar[j < n ? j : 0];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(av[j]));
+#pragma unroll
+        for (int j = 0; j < NP; ++j) an = j < n ? __builtin_fma(av[j], av[j], an) : an;
         const double sl = bv - row_dot(ar, n, xd);
         bad = sl < -feas_tol * (__builtin_sqrt(an) + __builtin_fabs(bv));
       }
