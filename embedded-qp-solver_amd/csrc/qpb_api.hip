@@ -390,4 +390,4 @@ extern "C" const char *qpb_last_error(void) { return g_err; }
 
 // the hot kernel revision is part of the string: profiles/pmc_traffic.json is
 // only trusted for the revision it was measured on (bench.py)
-extern "C" const char *qpb_version(void) { return "qpb 0.6 (gfx950; gi_dense v8: DPP-fused fmac sweep, in-sweep slacks, exact ratio step, one-trip loads, fp32-key select, 3 waves/SIMD; gi_box v1: lb <= x <= ub, A implicit; gi_wave v2: one-trip A gather for x, 32-bit key select, 3 waves/SIMD; gi_gram n<=128 on fp64 MFMA; ref v2: parallel independent sums)"; }
+extern "C" const char *qpb_version(void) { return "qpb 0.7 (gfx950; gi_dense v8.1: DPP-fused fmac sweep, in-sweep slacks, exact ratio step, one-trip loads and x gather, fp32-key select, 3 waves/SIMD; gi_box v1: lb <= x <= ub, A implicit; gi_wave v3: one-trip A gather for x, 32-bit key select, split setup sweep, 3 waves/SIMD; gi_gram v3 n<=128 on fp64 MFMA, broadcast row products, one-trip loads; ref v2: parallel independent sums)"; }
