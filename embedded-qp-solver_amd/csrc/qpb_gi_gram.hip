@@ -43,6 +43,9 @@
 #include "qpb_common.h"
 #include "qpb.h"
 
+#ifndef GRAM_PUB_ROWS
+#define GRAM_PUB_ROWS 0  // 1: every wave publishes its candidate row (session-4 form)
+#endif
 #ifndef GRAM_BC
 #define GRAM_BC 1
 #endif
@@ -648,6 +651,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       key = row_min(key);  // the 16 rows of each tile pair, on every lane group
       if (l == 0) red[R_KEY + wv] = key;
       const int pw = key_index256(key);
+#if GRAM_PUB_ROWS
       if (key < kBig) {
 #pragma unroll
         for (int t = 0; t < RT; ++t)
@@ -661,6 +665,14 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
             if (lk == 0) lds[B_CSP + wv] = s[t];
           }
       }
+#else
+      // the row itself is written after the selection, by its wave only
+      if (key < kBig) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+          if (row[t] == pw && lk == 0) lds[B_CSP + wv] = s[t];
+      }
+#endif
     };
     if (tid < NB) {
       iamb[tid] = -1;
@@ -679,9 +691,29 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           break;
         }
         p = key_index256(kmin);
-        ub = lds + B_CAND + (p / (16 * RT)) * PV;
         up = 0.0;
         selecting = false;
+#if GRAM_PUB_ROWS
+        ub = lds + B_CAND + (p / (16 * RT)) * PV;
+#else
+        // u = D[p,:] from the one wave that holds row p (an extra barrier is
+        // cheap; eight waves each storing a candidate row through four lanes
+        // kept the LDS store path busy)
+        ub = lds + B_CAND;
+        if (wv == p / (16 * RT)) {
+#pragma unroll
+          for (int t = 0; t < RT; ++t)
+            if (row[t] == p) {
+              double *dst = lds + B_CAND + 34 * lk;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                *reinterpret_cast<double2 *>(&dst[4 * k]) = make_double2(E[t][k][0], E[t][k][1]);
+                *reinterpret_cast<double2 *>(&dst[4 * k + 2]) = make_double2(E[t][k][2], E[t][k][3]);
+              }
+            }
+        }
+        __syncthreads();
+#endif
         double vr[RT];
         row_dot(E, ub + 34 * lk, vr);  // v = D u: column p of G
         if (lk == 0) {
