@@ -55,3 +55,15 @@ def test_valu_ceiling(bench):
     # 3000 instructions x 4 cycles x 256 waves per SIMD at 2.4 GHz
     assert v["ceiling_ms"] == pytest.approx(3000 * 4 * 256 / 2.4e9 * 1e3)
     assert v["frac"] == pytest.approx(v["ceiling_ms"] / 2.0)
+
+
+def test_committed_pmc_matches_the_built_library(bench):
+    # the bench line's roofline.traffic and valu_ceiling come from the committed
+    # PMC file only while it names the hot kernel revision the in-tree library
+    # reports; a kernel change without a new PMC pass must show up here
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
+    import qpb
+    t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    c = t["config"]
+    assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], c["family"], qpb.version()) is not None
