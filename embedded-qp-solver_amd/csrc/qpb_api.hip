@@ -257,9 +257,7 @@ static int check_ref(const qpb_ref_desc *d) {
   if (d->batch < 0 || d->n < 1 || d->iterations < 0) return fail(QPB_ERR_INVALID_ARG, "bad n/batch/iterations");
   if (d->mode != QPB_REF_NEWTON && d->mode != QPB_REF_ADMM && d->mode != QPB_REF_GD)
     return fail(QPB_ERR_INVALID_ARG, "unknown ref mode %d", d->mode);
-  if (d->n > 64)
-    return fail(QPB_ERR_UNSUPPORTED, "qpb_ref_solve: n=%d > 64 (the replica keeps P, its LU and two scratch "
-                "matrices in one workgroup's LDS)", d->n);
+  if (d->n > QPB_MAX_N) return fail(QPB_ERR_UNSUPPORTED, "qpb_ref_solve: n=%d > %d", d->n, QPB_MAX_N);
   return 0;
 }
 
@@ -271,7 +269,8 @@ extern "C" int qpb_ref_solve(const qpb_ref_desc *d, const double *P, const doubl
   if (!P || !q || !x || (!x0 && d->mode != QPB_REF_ADMM)) return fail(QPB_ERR_INVALID_ARG, "P, q, x0, x required");
   rc = check_device();
   if (rc) return rc;
-  // one 64-thread workgroup per QP: at most 2^25 QPs per launch
+  // n <= 64: one 64-thread workgroup per QP, at most 2^25 QPs per launch
+  // (n > 64: a grid of one workgroup per CU walks the batch)
   const long long n = d->n, step = 1LL << 25;
   for (long long k0 = 0; k0 < d->batch; k0 += step) {
     qpb_ref_desc c = *d;
@@ -308,7 +307,7 @@ extern "C" int qpb_ref_solve_host(const qpb_ref_desc *d, const double *P, const 
 
 extern "C" int qpb_matrix_invert(int32_t n, int64_t batch, const double *P, double *Pinv, void *stream) {
   if (n < 1 || batch < 0) return fail(QPB_ERR_INVALID_ARG, "bad qpb_matrix_invert arguments");
-  if (n > 64) return fail(QPB_ERR_UNSUPPORTED, "qpb_matrix_invert: n=%d > 64", n);
+  if (n > QPB_MAX_N) return fail(QPB_ERR_UNSUPPORTED, "qpb_matrix_invert: n=%d > %d", n, QPB_MAX_N);
   if (batch == 0) return 0;
   if (!P || !Pinv) return fail(QPB_ERR_INVALID_ARG, "P and Pinv are required");
   int rc = check_device();
@@ -336,7 +335,7 @@ extern "C" int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const doub
 extern "C" int qpb_ref_generate(const qpb_ref_gen_desc *d, double *P, double *q, double *x0, void *stream) {
   if (!d) return fail(QPB_ERR_INVALID_ARG, "desc is NULL");
   if (d->n < 1 || d->batch < 0) return fail(QPB_ERR_INVALID_ARG, "n must be >= 1 and batch >= 0");
-  if (d->n > 64) return fail(QPB_ERR_UNSUPPORTED, "qpb_ref_generate: n=%d > 64", d->n);
+  if (d->n > QPB_MAX_N) return fail(QPB_ERR_UNSUPPORTED, "qpb_ref_generate: n=%d > %d", d->n, QPB_MAX_N);
   if (d->batch > (1LL << 25))  // one 64-thread workgroup per QP: 2^32 work-items per launch
     return fail(QPB_ERR_UNSUPPORTED, "batch > 2^25 QPs per generator call (split it with `first`)");
   if (d->batch > 0 && (!P || !q || !x0)) return fail(QPB_ERR_INVALID_ARG, "NULL output pointer");

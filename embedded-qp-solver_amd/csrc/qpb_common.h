@@ -193,6 +193,27 @@ __device__ __forceinline__ void fmac_bc_nop(double &acc, double src, double mul)
 
 // exact min over the 16 lanes of the row (v_min_f64 on row_ror moves)
 __device__ __forceinline__ double row_min_exact(double v) { return row_min(v); }
+
+// The same without the canonicalising v_max_f64 that fmin() adds behind every
+// DPP move (4 fp64 instructions per reduction).  Operands are finite or
+// +-inf (never NaN) wherever it is used.
+__device__ __forceinline__ double fmin_raw(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double row_min_raw(double v) {
+  v = fmin_raw(v, ror<8>(v));
+  v = fmin_raw(v, ror<4>(v));
+  v = fmin_raw(v, ror<2>(v));
+  v = fmin_raw(v, ror<1>(v));
+  return v;
+}
+
+// Two wait states after the VALU instruction that produced `v`, before a run of
+// fmac_bc reads it through DPP (hipcc does not pad hazards around inline asm).
+// Taking v as an operand pins its producer above the s_nop.
+__device__ __forceinline__ void dpp_ready(double v) { asm volatile("s_nop 1" ::"v"(v)); }
 // min of a 32-bit value over the 16 lanes of the row (DPP-fused v_min_u32)
 __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
   v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kRowRor + 8, 0xF, 0xF, true));
@@ -210,10 +231,20 @@ __device__ __forceinline__ int wave_max4(int v) {
   const int ab = a > b ? a : b, cd = c > d ? c : d;
   return ab > cd ? ab : cd;
 }
+__device__ __forceinline__ int wave_min4(int v) {
+  const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  const int ab = a < b ? a : b, cd = c < d ? c : d;
+  return ab < cd ? ab : cd;
+}
 
 // Diagnostic builds only (STAMP = true, qpb_solve_sections): s_memrealtime stamps
 // (100 MHz) accumulate each wave's ticks per kernel section; the real kernels have none.
+// A wave adds its counters into the row (blockIdx.x mod kSectionSlots) of a
+// kSectionSlots x kSections buffer: one shared row made the flush atomics of a
+// 262,144-wave launch serialise on 20 addresses (a 30x longer stamped kernel).
 constexpr int kSections = 20;
+constexpr int kSectionSlots = 256;
 template <bool ON>
 struct SectionClock {
   __device__ __forceinline__ void tick(int) {}
@@ -239,8 +270,10 @@ struct SectionClock<true> {
     last = t;
   }
   __device__ __forceinline__ void flush(unsigned long long *dbg) {
-    if ((threadIdx.x & 63) == 0)
-      for (int i = 0; i < kSections; ++i) atomicAdd(&dbg[i], acc[i]);
+    if ((threadIdx.x & 63) == 0) {
+      unsigned long long *row = dbg + (size_t)(blockIdx.x % kSectionSlots) * kSections;
+      for (int i = 0; i < kSections; ++i) atomicAdd(&row[i], acc[i]);
+    }
   }
 };
 

@@ -126,10 +126,11 @@ __global__ __launch_bounds__(64) void ref_draws_kernel(int n, long long batch, u
   }
 }
 
-// one wave per QP: P <- B^T B / (pmax n), the reference's operation order
-// (k ascending, product rounded then added: matrix_mult :235-271, compiled
-// with -ffp-contract=off like the reference build)
-__global__ __launch_bounds__(64) void ref_posdef_kernel(int n, long long batch, double pmax,
+// one workgroup per QP (64 threads; 256 when n > 64): P <- B^T B / (pmax n),
+// the reference's operation order (k ascending, product rounded then added:
+// matrix_mult :235-271, compiled with -ffp-contract=off like the reference
+// build)
+__global__ __launch_bounds__(256) void ref_posdef_kernel(int n, long long batch, double pmax,
                                                         double *__restrict__ P) {
   extern __shared__ double Bs[];
   const long long k = blockIdx.x;
@@ -270,7 +271,13 @@ extern "C" hipError_t qpb_launch_ref_generate(int n, long long batch, unsigned l
                      range[1], range[2], range[3], range[4], range[5], P, q, x0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(qpb::gen::ref_posdef_kernel, dim3((unsigned)batch), dim3(64), n * n * sizeof(double), stream, n,
+  const size_t lds = (size_t)n * n * sizeof(double);  // B of one QP (n = 128: 128 KiB)
+  if (lds > 64 * 1024) {
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&qpb::gen::ref_posdef_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(qpb::gen::ref_posdef_kernel, dim3((unsigned)batch), dim3(n > 64 ? 256 : 64), lds, stream, n,
                      batch, range[1], P);
   return hipGetLastError();
 }

@@ -950,6 +950,8 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 }  // namespace gram
 }  // namespace qpb
 
+extern "C" hipError_t qpb_workspace(hipStream_t stream, size_t bytes, void **out);
+
 // scratch: per workgroup (NB - QL) D_W rows beyond the LDS ones + the queue head
 extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
                                          const double *b, double *x, double *lam, uint32_t *active,
@@ -965,7 +967,7 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
   const long long grid = d->batch < cus ? d->batch : cus;
   const size_t rows_bytes = (size_t)grid * qpb::gram::SCRATCH * sizeof(double);
   void *buf = nullptr;
-  e = hipMallocAsync(&buf, rows_bytes + 256, stream);
+  e = qpb_workspace(stream, rows_bytes + 256, &buf);  // cached per stream (qpb_workspace.hip)
   if (e != hipSuccess) return e;
   int *queue = reinterpret_cast<int *>(static_cast<char *>(buf) + rows_bytes);
   e = hipMemsetAsync(queue, 0, sizeof(int), stream);
@@ -980,6 +982,5 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
                          queue, static_cast<double *>(buf), nullptr);
     e = hipGetLastError();
   }
-  const hipError_t e2 = hipFreeAsync(buf, stream);
-  return e != hipSuccess ? e : e2;
+  return e;
 }

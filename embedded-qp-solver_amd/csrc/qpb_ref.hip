@@ -14,23 +14,29 @@
 // (gcc -O2, x86-64, no FMA) rounds every product and every sum, and so do
 // these kernels, in the same order.
 //
-// Layout: one QP per 64-thread workgroup; thread i owns row i (n <= 64).
-// LDS: P, the inverse, two n x n scratch matrices for the per-column solves
+// Layout: thread i owns row i.  n <= 64: one QP per 64-thread workgroup, P,
+// the LU / inverse and two n x n scratch matrices for the per-column solves
 // (thread t keeps its column's vectors in column t: conflict-free) and the
-// n-vectors.
+// n-vectors in LDS.  64 < n <= 128 (the reference's N_DIM is any compile-time
+// size; SURVEY §6 times refC at n = 128): 128-thread workgroups, P and the
+// vectors in LDS (<= 141 KB), the LU and the two scratch matrices in a global
+// workspace slice per workgroup (cached per stream, qpb_workspace.hip), and a
+// grid of one workgroup per CU walking the batch.  The arithmetic is the same
+// code in the same order either way.
 #include "qpb_common.h"
 #include "qpb.h"
 
 namespace qpb {
 
-constexpr int REF_MAXN = 64;
-constexpr int REF_THREADS = 64;
+constexpr int REF_MAXN = 128;
+constexpr int REF_LDS_MAXN = 64;  // n above this: matrices M, W, V in global memory
 
 struct RefShared {
   double *P, *M, *W, *V;  // n*n each (M: LU then inverse is V)
   double *x, *g, *d, *t0, *t1, *t2;  // n each
   double *scal;                       // scalars broadcast by thread 0
-  int *perm;
+  double *red;                        // cross-wave reduction slots (2)
+  int *perm, *redi;
 };
 
 // prod_i = sum_k A[i][k] * v[k], k ascending (matrix_mult, matrix_ops.c:262-270)
@@ -60,6 +66,8 @@ __device__ __forceinline__ double seq_norm(const double *a, int n) {
 
 // In-place explicit inverse of S.M (n x n), result in S.V (matrix_invert,
 // matrix_ops.c:551-630).  Thread i: row i in the LU, column i in the solves.
+// NT threads (64: one wavefront; 128: two, reduced through LDS).
+template <int NT>
 __device__ void ref_invert(RefShared &S, int n) {
   const int tid = threadIdx.x;
   if (tid < n) S.perm[tid] = tid;
@@ -67,8 +75,8 @@ __device__ void ref_invert(RefShared &S, int n) {
   bool singular = false;
   for (int k = 0; k + 1 < n; ++k) {  // matrix_lup_decompose :507
     // matrix_lup_pivot :449-470: the first row attaining the largest |M[i][k]|
-    // (a strict `>` scan from piv = 0), found by a wave-wide exact max and the
-    // lowest lane holding it (one workgroup = one wavefront)
+    // (a strict `>` scan from piv = 0), found by an exact max over the
+    // workgroup and the lowest thread holding it
     double v = 0.0;
     if (tid >= k && tid < n) {
       v = S.M[tid * n + k];
@@ -77,12 +85,22 @@ __device__ void ref_invert(RefShared &S, int n) {
     double piv = v;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) piv = __builtin_fmax(piv, __shfl_xor(piv, off));
+    if constexpr (NT > 64) {
+      if ((tid & 63) == 0) S.red[tid >> 6] = piv;
+      __syncthreads();
+      piv = __builtin_fmax(S.red[0], S.red[1]);
+    }
     if (!(piv > 0.0)) {  // singular: the reference prints and returns (:511-515)
       singular = true;
       break;
     }
     const unsigned long long hit = __ballot(tid >= k && tid < n && v == piv);
-    const int pidx = __builtin_ctzll(hit);
+    int pidx = __builtin_ctzll(hit);
+    if constexpr (NT > 64) {
+      if ((tid & 63) == 0) S.redi[tid >> 6] = hit ? (tid & ~63) + pidx : 1 << 30;
+      __syncthreads();
+      pidx = S.redi[0] < S.redi[1] ? S.redi[0] : S.redi[1];
+    }
     if (tid == 0) {  // permutation_swap :434-447
       const int tmp = S.perm[pidx];
       S.perm[pidx] = S.perm[k];
@@ -188,22 +206,39 @@ __device__ double ref_line_search(RefShared &S, const double *q, int n) {
   return alpha;
 }
 
-__global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long long batch, int iterations,
-                                                          double box_min, double box_max,
-                                                          const double *__restrict__ Pg, const double *__restrict__ qg,
-                                                          const double *__restrict__ x0g, double *__restrict__ xg,
-                                                          int32_t *__restrict__ itg) {
-  extern __shared__ double sm[];
-  const long long g = blockIdx.x;
-  if (g >= batch) return;
+// LDS (and workspace) carving shared by the solver and the invert kernels:
+// n <= 64 everything in `sm`; otherwise P (solver only) and the vectors in
+// `sm`, M / W / V in `wsq` (3 n^2 doubles)
+template <int NT>
+__device__ __forceinline__ double *ref_carve(RefShared &S, double *sm, double *wsq, int n, bool with_p) {
+  const int nn2 = n * n;
+  double *cur = sm;
+  if (with_p) {
+    S.P = cur;
+    cur += nn2;
+  }
+  if constexpr (NT > 64) {
+    S.M = wsq;
+    S.W = wsq + nn2;
+    S.V = wsq + 2 * nn2;
+  } else {
+    S.M = cur;
+    S.W = cur + nn2;
+    S.V = cur + 2 * nn2;
+    cur += 3 * nn2;
+  }
+  return cur;
+}
+
+// One QP of the reference solvers (thread i owns row i)
+template <int NT>
+__device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long g, int iterations, double box_min,
+                              double box_max, const double *__restrict__ Pg, const double *__restrict__ qg,
+                              const double *__restrict__ x0g, double *__restrict__ xg, int32_t *__restrict__ itg) {
   const int tid = threadIdx.x;
   RefShared S;
   const int nn2 = n * n;
-  S.P = sm;
-  S.M = S.P + nn2;
-  S.W = S.M + nn2;
-  S.V = S.W + nn2;
-  S.x = S.V + nn2;
+  S.x = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * 3 * nn2 : nullptr, n, true);
   // n-vectors packed at stride n: the LDS per QP sets the occupancy
   // (n = 16: 9.6 KB, 16 workgroups per CU)
   S.g = S.x + n;
@@ -215,7 +250,9 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
   double *u = q + n;
   double *z = u + n;
   S.scal = z + n;
-  S.perm = reinterpret_cast<int *>(S.scal + 8);
+  S.red = S.scal + 8;
+  S.perm = reinterpret_cast<int *>(S.red + 2);
+  S.redi = S.perm + n;
   const double *Pq = Pg + g * (long long)nn2;
   for (int e = tid; e < nn2; e += blockDim.x) S.P[e] = Pq[e];
   if (tid < n) {
@@ -230,7 +267,7 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
     if (mode == QPB_REF_NEWTON) {  // hessian_inv = invert(copy(P)) (:115-117)
       for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = S.P[e];
       __syncthreads();
-      ref_invert(S, n);
+      ref_invert<NT>(S, n);
     }
     for (; it < iterations; ++it) {
       ref_grad(S, q, S.x, S.g, n);
@@ -260,7 +297,7 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
     __syncthreads();
     if (tid < n) S.M[tid * n + tid] = S.M[tid * n + tid] + rho;  // R = P + rho I (:285-291)
     __syncthreads();
-    ref_invert(S, n);  // R^{-1} in S.V (:292)
+    ref_invert<NT>(S, n);  // R^{-1} in S.V (:292)
     const double sq = __builtin_sqrt((double)n);
     // admm_update_x's right-hand side rho (z - u) - q (:146-159) is each
     // thread's own entry, so it is formed at the end of the previous
@@ -322,6 +359,21 @@ __global__ __launch_bounds__(REF_THREADS) void ref_kernel(int mode, int n, long 
   if (tid == 0 && itg) itg[g] = it;
 }
 
+// NT = 64: matrices in LDS, one workgroup per QP.  NT = 128: M, W, V in the
+// workgroup's slice of `ws`; the grid walks the batch.
+template <int NT>
+__global__ __launch_bounds__(NT) void ref_kernel(int mode, int n, long long batch, int iterations,
+                                                 double box_min, double box_max, const double *__restrict__ Pg,
+                                                 const double *__restrict__ qg, const double *__restrict__ x0g,
+                                                 double *__restrict__ xg, int32_t *__restrict__ itg,
+                                                 double *__restrict__ ws) {
+  extern __shared__ double sm[];
+  for (long long g = blockIdx.x; g < batch; g += gridDim.x) {
+    ref_solve_one<NT>(sm, ws, mode, n, g, iterations, box_min, box_max, Pg, qg, x0g, xg, itg);
+    __syncthreads();  // LDS and workspace are reused by the next QP
+  }
+}
+
 // f(x) = 1/2 x^T (P x) + q^T x + r with the reference's order of operations:
 // tmp = matrix_mult(P, x) (sequential k), 0.5 * scalar_prod(x, tmp), + q.x, + r.
 __global__ void qf_eval_kernel(int n, long long batch, const double *__restrict__ P, const double *__restrict__ q,
@@ -347,42 +399,80 @@ __global__ void qf_eval_kernel(int n, long long batch, const double *__restrict_
 
 // Batched matrix_invert (matrix_ops.c:551-630) on its own: P -> P^{-1} per
 // QP, the same LU + per-column solves the Newton / ADMM replicas run.
-__global__ __launch_bounds__(REF_THREADS) void ref_invert_kernel(int n, long long batch,
-                                                                 const double *__restrict__ Pg,
-                                                                 double *__restrict__ Vg) {
+template <int NT>
+__global__ __launch_bounds__(NT) void ref_invert_kernel(int n, long long batch, const double *__restrict__ Pg,
+                                                        double *__restrict__ Vg, double *__restrict__ ws) {
   extern __shared__ double sm[];
-  const long long g = blockIdx.x;
-  if (g >= batch) return;
   const int tid = threadIdx.x;
   const int nn2 = n * n;
-  RefShared S;
-  S.P = nullptr;
-  S.M = sm;
-  S.W = S.M + nn2;
-  S.V = S.W + nn2;
-  S.scal = S.V + nn2;
-  S.perm = reinterpret_cast<int *>(S.scal + 8);
-  const double *Pq = Pg + g * (long long)nn2;
-  for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = Pq[e];
-  __syncthreads();
-  ref_invert(S, n);
-  double *Vq = Vg + g * (long long)nn2;
-  for (int e = tid; e < nn2; e += blockDim.x) Vq[e] = S.V[e];
+  for (long long g = blockIdx.x; g < batch; g += gridDim.x) {
+    RefShared S;
+    S.P = nullptr;
+    S.scal = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * 3 * nn2 : nullptr, n, false);
+    S.red = S.scal + 8;
+    S.perm = reinterpret_cast<int *>(S.red + 2);
+    S.redi = S.perm + n;
+    const double *Pq = Pg + g * (long long)nn2;
+    for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = Pq[e];
+    __syncthreads();
+    ref_invert<NT>(S, n);
+    double *Vq = Vg + g * (long long)nn2;
+    for (int e = tid; e < nn2; e += blockDim.x) Vq[e] = S.V[e];
+    __syncthreads();
+  }
 }
 
 }  // namespace qpb
 
+extern "C" hipError_t qpb_workspace(hipStream_t stream, size_t bytes, void **out);
+
+namespace {
+// LDS bytes of one workgroup: [P n^2] [M W V 3 n^2 when n <= 64] + 9 vectors
+// + 8 scalars + 2 reduction slots (doubles), perm + 2 (ints)
+size_t ref_lds_bytes(int n, bool with_p) {
+  const size_t nn2 = (size_t)n * n;
+  const size_t mats = (with_p ? nn2 : 0) + (n <= qpb::REF_LDS_MAXN ? 3 * nn2 : 0);
+  return sizeof(double) * (mats + 9 * (size_t)n + 10) + sizeof(int) * ((size_t)n + 2);
+}
+// n > 64: one workgroup per CU walks the batch, each with its 3 n^2 slice
+hipError_t ref_big_grid(long long batch, int n, hipStream_t stream, unsigned *grid, double **ws) {
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  *grid = (unsigned)(batch < cus ? batch : cus);
+  void *p = nullptr;
+  e = qpb_workspace(stream, (size_t)*grid * 3 * (size_t)n * n * sizeof(double), &p);
+  *ws = static_cast<double *>(p);
+  return e;
+}
+template <class K>
+hipError_t allow_lds(K kern, size_t lds) {
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds <= 64 * 1024) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds);
+}
+}  // namespace
+
 extern "C" hipError_t qpb_launch_ref_invert(int n, long long batch, const double *P, double *Pinv,
                                             hipStream_t stream) {
   if (n > qpb::REF_MAXN) return hipErrorInvalidValue;
-  const size_t lds = sizeof(double) * (3 * (size_t)n * n + 8) + sizeof(int) * ((size_t)n + 2);
-  if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&qpb::ref_invert_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (batch == 0) return hipSuccess;
+  const size_t lds = ref_lds_bytes(n, false);
+  if (n <= qpb::REF_LDS_MAXN) {
+    hipError_t e = allow_lds(&qpb::ref_invert_kernel<64>, lds);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(qpb::ref_invert_kernel<64>, dim3((unsigned)batch), dim3(64), lds, stream, n, batch, P, Pinv,
+                       nullptr);
+  } else {
+    unsigned grid = 0;
+    double *ws = nullptr;
+    hipError_t e = ref_big_grid(batch, n, stream, &grid, &ws);
+    if (e == hipSuccess) e = allow_lds(&qpb::ref_invert_kernel<128>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(qpb::ref_invert_kernel<128>, dim3(grid), dim3(128), lds, stream, n, batch, P, Pinv, ws);
   }
-  hipLaunchKernelGGL(qpb::ref_invert_kernel, dim3((unsigned)batch), dim3(qpb::REF_THREADS), lds, stream, n, batch, P,
-                     Pinv);
   return hipGetLastError();
 }
 
@@ -396,15 +486,22 @@ extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P
 extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q, const double *x0,
                                      double *x, int32_t *iters, hipStream_t stream) {
   if (d->n > qpb::REF_MAXN) return hipErrorInvalidValue;
+  if (d->batch == 0) return hipSuccess;
   const int n = d->n;
-  const size_t lds = sizeof(double) * (4 * (size_t)n * n + 10 * (size_t)n + 8) + sizeof(int) * ((size_t)n + 2);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&qpb::ref_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const size_t lds = ref_lds_bytes(n, true);
+  if (n <= qpb::REF_LDS_MAXN) {
+    hipError_t e = allow_lds(&qpb::ref_kernel<64>, lds);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(qpb::ref_kernel<64>, dim3((unsigned)d->batch), dim3(64), lds, stream, d->mode, n,
+                       (long long)d->batch, d->iterations, d->box_min, d->box_max, P, q, x0, x, iters, nullptr);
+  } else {
+    unsigned grid = 0;
+    double *ws = nullptr;
+    hipError_t e = ref_big_grid(d->batch, n, stream, &grid, &ws);
+    if (e == hipSuccess) e = allow_lds(&qpb::ref_kernel<128>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(qpb::ref_kernel<128>, dim3(grid), dim3(128), lds, stream, d->mode, n, (long long)d->batch,
+                       d->iterations, d->box_min, d->box_max, P, q, x0, x, iters, ws);
   }
-  hipLaunchKernelGGL(qpb::ref_kernel, dim3((unsigned)d->batch), dim3(qpb::REF_THREADS), lds, stream, d->mode, n,
-                     (long long)d->batch, d->iterations, d->box_min, d->box_max, P, q, x0, x, iters);
   return hipGetLastError();
 }

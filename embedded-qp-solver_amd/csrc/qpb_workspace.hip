@@ -1,0 +1,65 @@
+// qpb_workspace.hip -- cached device scratch for the kernels that need one
+// (the n <= 128 Gram kernel's spilled rows and work queue, the reference
+// replicas' matrices at 64 < n <= 128).
+//
+// One buffer per (device, stream), grown on demand and never shrunk: a solve
+// reuses it instead of a hipMallocAsync / hipFreeAsync pair per call.  Work on
+// one stream runs in order, so a buffer handed to consecutive launches on the
+// same stream is never used by two of them at once; different streams get
+// different buffers.  Growing frees the old buffer stream-ordered (after the
+// launches already queued on that stream).  qpb_release_workspaces() returns
+// everything (e.g. before hipDeviceReset).
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+namespace {
+struct Entry {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_mu;
+std::map<std::pair<int, hipStream_t>, Entry> g_ws;
+}  // namespace
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t qpb_workspace(hipStream_t stream, size_t bytes,
+                                                                          void **out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(g_mu);
+  Entry &w = g_ws[{dev, stream}];
+  if (w.bytes < bytes) {
+    if (w.p) (void)hipFreeAsync(w.p, stream);
+    w = Entry{};
+    // round up to 1 MiB so that a slowly growing batch does not reallocate every call
+    const size_t want = (bytes + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+    e = hipMallocAsync(&w.p, want, stream);
+    if (e != hipSuccess) {
+      w = Entry{};
+      return e;
+    }
+    w.bytes = want;
+  }
+  *out = w.p;
+  return hipSuccess;
+}
+
+extern "C" int qpb_release_workspaces(void) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  int failed = 0;
+  for (auto &kv : g_ws) {
+    if (!kv.second.p) continue;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(kv.first.first);
+    if (hipFreeAsync(kv.second.p, kv.first.second) != hipSuccess ||
+        hipStreamSynchronize(kv.first.second) != hipSuccess)
+      ++failed;
+    (void)hipSetDevice(cur);
+  }
+  g_ws.clear();
+  return failed ? -3 : 0;  // QPB_ERR_HIP
+}

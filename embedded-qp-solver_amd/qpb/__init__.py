@@ -173,6 +173,8 @@ def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, feas_tol: float = 0.
     for t in (H, f, lb, ub):
         if t is not None and (t.dtype != torch.float64 or not t.is_contiguous()):
             raise ValueError("inputs must be contiguous float64")
+        if t is not None and t.device != f.device:
+            raise ValueError("H, f, lb and ub must live on the same CUDA device")
     if H.shape != (B, n, n) or any(t is not None and t.shape != (B, n) for t in (lb, ub)):
         raise ValueError("shape mismatch")
     dev = f.device
@@ -242,6 +244,9 @@ def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), s
 def matrix_invert(P, stream=None):
     """Batched reference matrix_invert (matrix_ops.c:551-630) of (B, n, n) CUDA tensors."""
     import torch
+    if not (P.is_cuda and P.dtype == torch.float64 and P.is_contiguous() and P.dim() == 3
+            and P.shape[1] == P.shape[2]):
+        raise ValueError("qpb.matrix_invert expects a contiguous float64 CUDA tensor of shape (B, n, n)")
     B, n, _ = P.shape
     out = torch.empty_like(P)
     _check(_lib.qpb_matrix_invert(n, B, _ptr(P), _ptr(out), _stream_ptr(stream)), "qpb_matrix_invert")
@@ -261,6 +266,8 @@ _lib.qpb_solve_sections.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 11
 _lib.qpb_solve_sections.restype = ctypes.c_int
 SECTION_NAMES = ["load", "cholesky", "substitution", "init", "select", "exchange", "back_solve", "step",
                  "add", "drop", "loop_exit", "output"]
+N_SECTIONS = 20  # kSections (csrc/qpb_common.h): every stamped kernel adds all of them into the buffer
+SECTION_SLOTS = 256  # kSectionSlots: rows of the device buffer (one per blockIdx mod 256)
 WAVE_SECTION_NAMES = ["load", "sweep", "init", "select", "exchange", "back_solve", "step", "add", "drop",
                       "loop_exit", "x", "stores"]
 
@@ -268,17 +275,23 @@ WAVE_SECTION_NAMES = ["load", "sweep", "init", "select", "exchange", "back_solve
 def solve_sections(H, f, A, b, sections, *, max_iter: int = 0, out: Solution | None = None, stream=None):
     """Diagnostic builds of the n=16 (16<m<=32) and 16<n<=32 (m<=64) kernels:
     accumulate per-section wave ticks (100 MHz) into the int64 CUDA tensor
-    ``sections`` (12 entries: SECTION_NAMES / WAVE_SECTION_NAMES)."""
+    ``sections`` (N_SECTIONS = 20 int64 entries; the first 12 are named by
+    SECTION_NAMES / WAVE_SECTION_NAMES)."""
     import torch
+    if not (sections.is_cuda and sections.dtype == torch.int64 and sections.is_contiguous()
+            and sections.numel() >= N_SECTIONS):
+        raise ValueError(f"sections must be a contiguous int64 CUDA tensor of >= {N_SECTIONS} entries")
     B, n = f.shape
     m = A.shape[1]
     if out is None:
         out = solve(H, f, A, b, max_iter=max_iter, stream=stream)
     d = Desc(n, m, B, max_iter, 0, 0.0)
+    rows = torch.zeros((SECTION_SLOTS, N_SECTIONS), dtype=torch.int64, device=sections.device)
     rc = _lib.qpb_solve_sections(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(A), _ptr(b), _ptr(out.x), _ptr(out.lam),
-                                 _ptr(out.active), _ptr(out.status), _ptr(out.iters), _ptr(sections),
+                                 _ptr(out.active), _ptr(out.status), _ptr(out.iters), _ptr(rows),
                                  _stream_ptr(stream))
     _check(rc, "qpb_solve_sections")
+    sections[:N_SECTIONS] += rows.sum(0)
     return out
 
 

@@ -181,7 +181,8 @@ int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
 
 /* Diagnostic: same solve (n = 16 with 16 < m <= 32, or 16 < n <= 32 with
  * m <= 64) by a build of the kernel with s_memrealtime stamps (100 MHz); adds
- * each wavefront's ticks per kernel section into sections[] (20 counters).
+ * each wavefront's ticks per kernel section into row (workgroup index mod 256)
+ * of sections[256][20] (zero it first; sum the rows for the totals).
  * n = 16: load, cholesky, substitution, init, select, exchange, back-solve,
  * step, add, drop, loop-exit, output.  16 < n <= 32: load, sweep, init,
  * select, exchange, back-solve, step, add, drop, loop-exit, x, stores. */
@@ -251,6 +252,10 @@ int qpb_wire_read(const char *path, double *H, double *f, double *A, double *b);
 int qpb_device_count(void);
 int qpb_set_device(int device);
 int qpb_synchronize(void *stream);
+/* Scratch buffers are cached per (device, stream) and reused across calls
+ * (the n <= 128 kernels and the reference replicas at n > 64 need one);
+ * this synchronises those streams and frees them all. */
+int qpb_release_workspaces(void);
 const char *qpb_last_error(void);
 const char *qpb_version(void);
 

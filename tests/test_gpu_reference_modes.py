@@ -112,7 +112,7 @@ def test_matrix_invert_bitwise(qpb, n):
 
 
 def test_matrix_invert_rejects_large_n(qpb):
-    P = torch.zeros((1, 65, 65), dtype=torch.float64, device="cuda")
+    P = torch.zeros((1, 129, 129), dtype=torch.float64, device="cuda")
     with pytest.raises(qpb.QPBError):
         qpb.matrix_invert(P)
 
@@ -120,18 +120,25 @@ def test_matrix_invert_rejects_large_n(qpb):
 REF_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref")
 
 
-@pytest.mark.parametrize("n", [4, 16, 32])
+@pytest.mark.parametrize("n", [4, 16, 32, 48, 128])
 def test_replicas_bitwise_vs_live_reference(qpb, n):
-    """256 fresh QPs from the reference generator per n, solved by the
-    compiled reference (oracle/_ref, linked -Bsymbolic so its internal calls
-    stay inside the reference) and by the GPU replicas: matrix_invert, Newton
-    (10 iterations) and ADMM (1e4, default and active box) bitwise equal."""
+    """Fresh QPs from the reference generator per n (256; 64 at n = 128, where
+    refC's ADMM takes ~60 ms per QP), solved by the compiled reference
+    (oracle/_ref, linked -Bsymbolic so its internal calls stay inside the
+    reference) and by the GPU replicas: matrix_invert, Newton (10 iterations)
+    and ADMM (1e4, default and active box) bitwise equal.  n = 48 is the
+    reference's own default (config.h:5); n > 64 runs the replicas' global-
+    workspace form (qpb_ref.hip)."""
     import refc
     if not refc.available(n, "1e12") or not refc.available(n, "1e2"):
         pytest.skip("oracle/_ref not built")
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     rc = refc.RefC(n, "1e12")
-    P, q, x0 = rc.generate(seed=4242 + n, count=256)
+    P, q, x0 = rc.generate(seed=4242 + n, count=64 if n > 64 else 256)
+    # the GPU generator replays the same reference sequence bit for bit
+    Pg, qg, xg = qpb.ref_generate(n, len(P), 4242 + n)
+    assert np.array_equal(Pg.cpu().numpy(), P) and np.array_equal(qg.cpu().numpy(), q)
+    assert np.array_equal(xg.cpu().numpy(), x0)
     inv_ref = np.stack([rc.invert(P[i].copy()) for i in range(len(P))])
     assert np.array_equal(qpb.matrix_invert(dev(P)).cpu().numpy(), inv_ref)
     x, _ = _run(qpb, qpb.REF_NEWTON, P, q, x0, 10)
@@ -141,6 +148,21 @@ def test_replicas_bitwise_vs_live_reference(qpb, n):
     ra = refc.RefC(n, "1e2")
     x, _ = _run(qpb, qpb.REF_ADMM, P, q, x0, 10000, box=(-1e2, 1e2))
     assert np.array_equal(x, ra.admm(P, q, x0, 10000))
+
+
+@pytest.mark.parametrize("n", [32])
+def test_gd_bitwise_vs_live_reference(qpb, n):
+    """REF_GD (qp_solvers.c:65-101, 1e4 iterations, ~57 Armijo trials each)
+    on fresh reference-generator QPs against the compiled reference; refC
+    takes ~0.5 s per QP at n = 32, so 8 QPs."""
+    import refc
+    if not refc.available(n, "1e12"):
+        pytest.skip("oracle/_ref not built")
+    rc = refc.RefC(n, "1e12")
+    P, q, x0 = rc.generate(seed=777 + n, count=8)
+    x, it = _run(qpb, qpb.REF_GD, P, q, x0, 10000)
+    assert np.array_equal(x, rc.gd(P, q, x0, 10000))
+    assert (it >= 1).all() and (it <= 10000).all()
 
 
 def test_qf_eval(qpb):

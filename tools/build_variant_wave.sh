@@ -10,6 +10,6 @@ cp "$src" csrc/zz_wvariant_$name.hip
 /opt/rocm/bin/hipcc -std=c++20 -O3 --offload-arch=gfx950 -fPIC -I../include -I../include/compat -Icsrc \
   -Wno-unused-function ${VFLAGS:-} -c csrc/zz_wvariant_$name.hip -o build/wvariant_$name.o
 rm -f csrc/zz_wvariant_$name.hip
-objs="build/qpb_gi_box.o build/qpb_gi.o build/qpb_gi_mixed.o build/qpb_gi_block.o build/qpb_gi_gram.o build/qpb_ref.o build/qpb_gen.o build/qpb_api.o build/compat.o build/qpb_wire.o"
+objs=$(ls build/qpb_*.o build/compat.o | grep -v "build/qpb_gi_wave.o")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,-Bsymbolic -o lib/libqpb_$name.so build/wvariant_$name.o $objs
 echo lib/libqpb_$name.so

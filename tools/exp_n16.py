@@ -51,7 +51,7 @@ out["iters_hist"] = torch.bincount(it).tolist()
 for w in (2, 4):
     mx = it[: (B // w) * w].view(-1, w).max(1).values.double()
     out[f"lockstep_trips_mean_{w}qp"] = float(mx.mean())
-sec = torch.zeros(12, dtype=torch.int64, device=dev)
+sec = torch.zeros(qpb.N_SECTIONS, dtype=torch.int64, device=dev)
 qpb.solve_sections(H, f, A, b, sec, out=sol)
 sec.zero_()
 a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -66,6 +66,10 @@ __global__ __launch_bounds__(64) void lat_kernel(double *out, double seed, long 
       a = sh[(threadIdx.x + 1) & 63] + 1.0;
     }
     if constexpr (KIND == 4) a = __builtin_amdgcn_rcp(a);
+    if constexpr (KIND == 5)  // accumulator chain of v_fmac_f64_dpp (the DPP source is a fixed register)
+      asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(a) : "v"(seed), "v"(0.999));
+    if constexpr (KIND == 6)  // the same chain on plain v_fmac_f64
+      asm volatile("v_fmac_f64 %0, %1, %2" : "+v"(a) : "v"(seed), "v"(0.999));
   }
   const long long t1 = clock64();
   out[blockIdx.x * 64 + threadIdx.x] = a;
@@ -125,7 +129,7 @@ int main() {
   thr(thr_kernel<7>, tn[7]);
   thr(thr_kernel<8>, tn[8]);
   const char *ln[] = {"fma_f64_dep", "mov_b64_dpp_dep", "dpp_ror+min_f64_dep", "ds_write+ds_read_f64_dep",
-                      "rcp_f64_dep"};
+                      "rcp_f64_dep", "fmac_f64_dpp_acc_dep", "fmac_f64_acc_dep"};
   auto lat = [&](auto kern, const char *name) {
     hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, 0, out, 1.0, clk);
     hipDeviceSynchronize();
@@ -138,6 +142,8 @@ int main() {
   lat(lat_kernel<2>, ln[2]);
   lat(lat_kernel<3>, ln[3]);
   lat(lat_kernel<4>, ln[4]);
+  lat(lat_kernel<5>, ln[5]);
+  lat(lat_kernel<6>, ln[6]);
   double *err;
   hipMalloc(&err, 2 * sizeof(double));
   hipMemset(err, 0, 2 * sizeof(double));
