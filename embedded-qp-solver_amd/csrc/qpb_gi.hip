@@ -16,59 +16,39 @@
 //           substitution of both D rows of lane l and the lane-parallel y.
 //           Slack of the unconstrained minimiser x0 = -H^{-1} f
 //           (test/qp_ref.py:35's answer): s = b - A x0 = b + D y.
-//   iterate pick the most violated row p (normalised slack, fp32 argmax key);
-//           d = -D[p,:] (= J^T n+ in G-I's notation, J = L^{-T} Q, n+ = -a_p),
-//           dual step r = R^{-1} d1 (lane-parallel back substitution),
-//           partial step t1 (ratio test over the active multipliers),
-//           full step t2 = -s_p / |d2|^2, slacks s -= t D[:, q:] d2;
+//   iterate D = A L^{-T} Q is kept in the rotated basis Q: the rows of the
+//           active constraints are zero on the free basis columns q..15.
+//           Pick the violated row p with the largest violation per unit
+//           length of its free part, -s_p / |D[p, q:]| (dual steepest edge;
+//           the squared free norms are kept up to date, fp32 keys); its row
+//           d = D[p,:] splits into d1 (columns < q) and d2 (columns >= q).
+//           Dual step r = R^{-1} d1 (lane-parallel back substitution over the
+//           prefetched R column), partial step t1 (ratio test over the active
+//           multipliers), full step t2 = -s_p / |d2|^2, slacks s -= t D d2.
 //           full step  -> ADD p: one Householder reflection on columns q..15
 //                         of D (every lane updates its own rows), new column
 //                         of R;
 //           partial    -> DROP k: delete column k of R, Givens rotations
 //                         restore triangularity (also applied to D).
-//           Row p travels through an LDS exchange row; the active columns are
-//           zeroed and the Householder vector formed IN LDS (one lane-masked
-//           store each), so no per-element selects run on the VALU.
 //   finish  x = -H^{-1} (f + A^T lam) from the final multipliers (KKT
-//           stationarity): the q active rows of A are re-read, two lane-
+//           stationarity): the active rows of A are re-read, two lane-
 //           parallel triangular solves with L kept in LDS.
 //
 // Data layout per QP (lane l = 0..15 of the QP's 16-lane DPP row):
 //   registers  rows l + 16 r (r < MR) of D, their slacks, 1/||a_row||,
-//              |D row|^2, active flags; multiplier / row of active position l
-//   LDS        L (packed rows, true diagonal) + 1/L_kk, R (16 x 18 padded rows,
-//              zero diagonal + separate diagonal), exchange row, Givens
-//              parameters, lambda scatter buffer.  The R area doubles as the
-//              staging buffer of the coalesced input transposes.
+//              |D row|^2, |free part|^2, active flags; multiplier / row of
+//              active position l, R[l][l] and its reciprocal
+//   LDS        L (packed rows), R (16 x 16 column-major, zero diagonal),
+//              exchange row, Givens parameters, lambda scatter buffer.  The R
+//              area doubles as the staging buffer of the coalesced input
+//              transposes.
+// Every product with a vector held one entry per lane (d2, the Householder
+// vector) is a v_fmac_f64_dpp reading the entry from lane j by row_newbcast:
+// no LDS round trip, no copy of the vector in every lane.
 // No branch or select compares the lane id with a compile-time constant:
 // such masks are hoisted by the compiler and end up spilled (SGPR pressure).
-// Values a lane produces for the whole row are captured by same-address LDS
-// stores from all 16 lanes instead.
 #include "qpb_common.h"
 #include "qpb.h"
-
-// A/B switches of the round-2 changes (all on in the shipped build)
-#ifndef QPB_DPPFMA
-#define QPB_DPPFMA 1  // broadcasts fused into v_fmac_f64_dpp (sweep, back substitution)
-#endif
-#ifndef QPB_DDINV
-#define QPB_DDINV 0  // |D[p,:]|^2 from the setup (invariant under the column rotations)
-#endif
-#ifndef QPB_ROWLOAD
-#define QPB_ROWLOAD 0  // each lane loads its own rows (no LDS transposes)
-#endif
-#ifndef QPB_SINC
-#define QPB_SINC 1  // s = b + D y accumulated inside the sweep (no y round trip through LDS)
-#endif
-#ifndef QPB_PF_DIST
-#define QPB_PF_DIST 0  // > 0: each wave prefetches the input lines of group blockIdx + QPB_PF_DIST
-#endif
-#ifndef QPB_XCH2
-#define QPB_XCH2 0  // 1: the owner lane writes both its D rows (no selects), s_p by a shuffle -- measured 5.7 % slower (profiles/r02/ab_xch.json)
-#endif
-#ifndef QPB_RATIO_MIN
-#define QPB_RATIO_MIN 1  // ratio test: exact f64 min + u32 argmin, no LDS round trip
-#endif
 
 namespace qpb {
 
@@ -83,17 +63,18 @@ __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
 constexpr int L_SIZE = lrow(NL);  // 136
 
 // LDS slot of one QP: 424 doubles = 3,392 B, 13,568 B per wave -> 12 waves
-// per CU (3 per SIMD, matching the 168-VGPR budget)
+// per CU (3 per SIMD, matching the VGPR budget)
 constexpr int OFF_L = 0;                  // L (136)
-constexpr int OFF_R = L_SIZE;             // R column-major, 16 x 16: R[i][j] at j*16 + i
-constexpr int OFF_XCH = OFF_R + NL * NL;  // 392: exchange row d (16), s_p, |d|^2; Givens
-                                          // cos / sin (16 + 16); y / x capture; lambda scatter
+constexpr int OFF_T = L_SIZE;             // R, column-major 16 x 16: R[i][j] at j*16 + i
+constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: exchange row d (16), s_p, |d|^2; Givens cos / sin
+                                          // (16 + 16); y / x capture; lambda scatter
 constexpr int SLOT = OFF_XCH + 32;        // 424
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
-// reciprocals and inverse square roots: hardware estimate + one Newton step
-// (rcp1 / rsq1, qpb_common.h)
-static_assert(SLOT % 2 == 0 && OFF_R % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
-static_assert(NL * RS <= SLOT - OFF_R, "input transposes are staged in R + xch");
+#ifndef QPB_RV_PREFETCH
+#define QPB_RV_PREFETCH 0  // R entries of the back substitution read ahead (multiple of 4, <= 16): 8 spills (+21 %)
+#endif
+static_assert(SLOT % 2 == 0 && OFF_T % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
+static_assert(NL * RS <= SLOT - OFF_T, "input transposes are staged in T + xch");
 
 // sum_{j<N} x(j) y(j) with 2 independent accumulators
 template <int N, class FX, class FY>
@@ -107,17 +88,6 @@ __device__ __forceinline__ double dot2(FX &&x, FY &&y, double init = 0.0) {
   return a0 + a1;
 }
 
-// ... and with 4 (shorter dependency chains in the active-set loop)
-template <int N, class FX, class FY>
-__device__ __forceinline__ double dot4(FX &&x, FY &&y) {
-  double a[4] = {0.0, 0.0, 0.0, 0.0};
-  unroll<N>([&](auto J) {
-    constexpr int j = J;
-    a[j % 4] = __builtin_fma(x(j), y(j), a[j % 4]);
-  });
-  return (a[0] + a[1]) + (a[2] + a[3]);
-}
-
 // 16 doubles from LDS (16-byte aligned) as 8 b128 reads
 __device__ __forceinline__ void lds_row16(const double *src, double (&dst)[NL]) {
 #pragma unroll
@@ -128,22 +98,37 @@ __device__ __forceinline__ void lds_row16(const double *src, double (&dst)[NL]) 
   }
 }
 
+// out[r] = sum_j vec[lane j] * x[r][j] over the row's 16 lanes, DPP-fused;
+// the MR rows interleaved, two chains each (2 MR independent accumulators);
+// the caller has issued dpp_ready(vec)
+template <int MR>
+__device__ __forceinline__ void bdot_rows(double vec, const double (&x)[MR][NL], double (&out)[MR]) {
+  double a[MR][2];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) a[r][0] = a[r][1] = 0.0;
+  unroll<NL>([&](auto J) {
+    constexpr int j = J;
+#pragma unroll
+    for (int r = 0; r < MR; ++r) fmac_bc<j>(a[r][j & 1], vec, x[r][j]);
+  });
+#pragma unroll
+  for (int r = 0; r < MR; ++r) out[r] = a[r][0] + a[r][1];
+}
 // MR: rows of D per lane (m <= 16 MR).  N16: n == 16 (coalesced loads).
 // FULL: n == 16 and m == 16 MR (no padding rows: no masking anywhere).
-// One group = the 4 QPs of a wavefront; `grp` its index, `nxt` the group
-// this wave solves next (< 0: none) -- its input lines are prefetched into
-// the caches while this group iterates (persistent launch).
+// One group = the 4 QPs of a wavefront; `grp` its index.
 template <int MR, bool N16, bool FULL, bool STAMP>
 __device__ __forceinline__ void gi_group(
     double *lds, const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
     uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
     long long batch, int max_iter, double feas_tol, int flags, unsigned long long *__restrict__ dbg,
-    long long grp, long long nxt) {
+    long long grp) {
   static_assert(!FULL || N16, "FULL implies n == 16");
   SectionClock<STAMP> clk;
   const int l = threadIdx.x & (NL - 1);
   const int slot = threadIdx.x >> 4;
+  const int sh = (threadIdx.x & 63) & ~(NL - 1);  // this row's bit offset in a wave ballot
   // Rows past the end of the batch (last group only) do not leave: they replay
   // the batch's last QP -- same trip count, so they never extend the wave's
   // loop -- and store nothing.  Every lane of the wave stays live, so the
@@ -162,23 +147,24 @@ __device__ __forceinline__ void gi_group(
   // 32 banks apart
   double *base = lds + (((slot & 1) << 1) | (slot >> 1)) * SLOT;
   double *Lp = base + OFF_L;
-  double *R = base + OFF_R;  // column-major
+  double *Tv = base + OFF_T;  // R, column-major (zero diagonal)
+  double *gcs = base + OFF_XCH;  // Givens cosines (DROP only)
+  double *gsn = gcs + NL;        // Givens sines
   double *xch = base + OFF_XCH;
-  double *gcs = xch;       // Givens cosines (DROP only)
-  double *gsn = xch + NL;  // Givens sines
 
   // ------------------------------------------------------------------ load
   // (flags & QPB_FLAG_DIAG_L2: every QP reads the inputs of QP g mod 512;
   // QPB_FLAG_DIAG_MALL: of QP g mod 16384 (107 MB, Infinity-Cache resident
   // after the first launch) -- diagnostics that take HBM out of the kernel time)
-  const long long gi = (flags & 1) ? (g & 511) : (flags & 16) ? (g & 16383) : g;
+  const long long gi = (flags & QPB_FLAG_DIAG_L2) ? (g & 511) : (flags & QPB_FLAG_DIAG_MALL) ? (g & 16383) : g;
   const double *Hq = Hg + gi * (long long)n * n;
   // m == 0: A/b may be NULL -- point the (masked) row loads at H instead
   const double *Aq = m > 0 ? Ag + gi * (long long)m * n : Hq;
   const double *bq = m > 0 ? bg + gi * (long long)m : Hq;
   double Lr[NL];  // row l of H, becomes row l of L
   double E[MR][NL];
-  double s[MR], invn[MR], bl[MR], thr[MR];
+  double s[MR], invn[MR], bl[MR], thr[MR], ddr[MR];
+  float fn2[MR];  // |D[r, q:]|^2, the free part of the row (scale of the selection key)
   bool act[MR];
   bool infeasible_row = false;
   // b and f with the matrices (same round trip)
@@ -186,48 +172,11 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
   for (int r = 0; r < MR; ++r) bv[r] = bq[(FULL || l + NL * r < m) ? l + NL * r : 0];
   const double fv = fg[gi * n + (l < n ? l : n - 1)];
-  if constexpr (N16 && QPB_ROWLOAD) {
-    // Each lane loads the rows it owns -- H row l, A rows l and l + 16 -- as
-    // eight 16-byte pieces each, straight into registers: every 128-B row is
-    // one cache line, read whole by the lane's 8 loads; no LDS transposes.
-    // All loads are issued at once (one HBM round trip); an empty asm
-    // consumes them right here, since instruction selection would otherwise
-    // sink each load to its first use.
-    double2 hv[8], av[MR][8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) hv[t] = *reinterpret_cast<const double2 *>(&Hq[l * NL + 2 * t]);
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      const int row = l + NL * r;
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-        av[r][t] = (FULL || row < m) ? *reinterpret_cast<const double2 *>(&Aq[row * NL + 2 * t])
-                                     : make_double2(0.0, 0.0);
-    }
-#pragma unroll
-    for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(bv[r]));
-    asm volatile("" ::"v"(fv));
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      asm volatile("" ::"v"(hv[t].x), "v"(hv[t].y));
-#pragma unroll
-      for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(av[r][t].x), "v"(av[r][t].y));
-    }
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      Lr[2 * t] = hv[t].x;
-      Lr[2 * t + 1] = hv[t].y;
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        E[r][2 * t] = av[r][t].x;
-        E[r][2 * t + 1] = av[r][t].y;
-      }
-    }
-  } else if constexpr (N16) {
+  if constexpr (N16) {
     // Coalesced 16-byte loads: one instruction reads 2 whole rows (256 B) of
     // each of the wave's 4 QPs -- lane l gets row 2t + (l>>3), columns
     // 2(l&7), 2(l&7)+1.  Rows reach their owner lane through a transpose in
-    // this QP's R region of LDS (free until the active-set loop).
+    // this QP's T region of LDS (free until the active-set loop).
     const int hr = l >> 3, hc = 2 * (l & 7);
     double2 hv[8];
 #pragma unroll
@@ -245,9 +194,9 @@ __device__ __forceinline__ void gi_group(
     auto transpose = [&](const double2 (&v)[8], double (&dst)[NL]) {
       wave_lds_sync();
 #pragma unroll
-      for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&R[(2 * t + hr) * RS + hc]) = v[t];
+      for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&Tv[(2 * t + hr) * RS + hc]) = v[t];
       wave_lds_sync();
-      lds_row16(&R[l * RS], dst);
+      lds_row16(&Tv[l * RS], dst);
     };
     // all input rows in flight at once (one HBM round trip); instruction
     // selection sinks loads to their first use, so an empty asm consumes
@@ -310,21 +259,19 @@ __device__ __forceinline__ void gi_group(
   //   D rows: E[k] /= sqrt(akk), E[j] -= E[k] pr[j] / akk (j > k)
   //   y:      lane-parallel, f_l -= c f_k;  y_k = f_k / sqrt(akk)
   // Lanes l < k keep updating dead entries of their row (the upper triangle,
-  // never read); y_k and 1/L_kk are captured by same-address LDS stores.
+  // never read).  The pivot row is read straight from lane k by the FMAs
+  // (v_fmac_f64_dpp); the sched_barrier and the rsq chain keep every write of
+  // Lr[j] (previous step) well over two instructions before these reads.
+  // Lane k's own Lr[j] is updated last, after the D rows have read it.
+  // s = b + D y accumulates in the same sweep (D[:, k] and y_k are final at
+  // step k).
   bool spd = true;
   double ya = fl;
-#if QPB_SINC
 #pragma unroll
   for (int r = 0; r < MR; ++r) s[r] = bl[r];
-#endif
   unroll<NL>([&](auto K) {
     constexpr int k = K;
     __builtin_amdgcn_sched_barrier(0);
-#if QPB_DPPFMA
-    // the pivot row is read straight from lane k by the FMAs (v_fmac_f64_dpp);
-    // the sched_barrier above and the rsq chain below keep every write of
-    // Lr[j] (previous step) well over two instructions before these reads.
-    // Lane k's own Lr[j] is updated last, after the D rows have read it.
     const double akk = bc<k>(Lr[k]);
     spd = spd && (akk > 0.0);
     const double ik = rsq1(akk);
@@ -345,40 +292,11 @@ __device__ __forceinline__ void gi_group(
     });
     Lr[k] *= ik;
     const double c = -nc;
-#else
-    double pr[NL];
-    unroll<NL - k>([&](auto J) { pr[k + J] = bc<k>(Lr[k + J]); });
-    const double akk = pr[k];
-    spd = spd && (akk > 0.0);
-    const double ik = rsq1(akk);
-    const double ik2 = ik * ik;
-    const double c = Lr[k] * ik2;
-    unroll<NL - 1 - k>([&](auto J) {
-      constexpr int j = k + 1 + J;
-      Lr[j] = __builtin_fma(-c, pr[j], Lr[j]);
-    });
-    Lr[k] *= ik;
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      const double e = E[r][k];
-      const double e2 = e * ik2;
-      E[r][k] = e * ik;
-      unroll<NL - 1 - k>([&](auto J) {
-        constexpr int j = k + 1 + J;
-        E[r][j] = __builtin_fma(-e2, pr[j], E[r][j]);
-        pin(E[r][j]);
-      });
-    }
-#endif
     const double fk = bc<k>(ya);
     ya = __builtin_fma(-c, fk, ya);
-#if QPB_SINC
     const double yk = fk * ik;  // y_k; D[r][k] is final now
 #pragma unroll
     for (int r = 0; r < MR; ++r) s[r] = __builtin_fma(E[r][k], yk, s[r]);
-#else
-    xch[k] = fk * ik;  // y_k
-#endif
   });
   __builtin_amdgcn_sched_barrier(0);
   // L -> LDS, packed rows (lane l writes row l), kept for the final solves.
@@ -390,33 +308,22 @@ __device__ __forceinline__ void gi_group(
     Lp[lrow(l) + j] = Lr[j];
     wave_lds_sync();
   });
-#if !QPB_SINC
-  {
-    double yv[NL];
-    lds_row16(xch, yv);
+  // |D[r,:]|^2 = |a_r L^{-T}|^2: the loop's reflections are orthogonal, so it
+  // never changes (the dependency test's scale)
 #pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      s[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return yv[j]; }, bl[r]);
-    }
+  for (int r = 0; r < MR; ++r) {
+    ddr[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
+    fn2[r] = (float)ddr[r];
   }
-#endif
-#if QPB_DDINV
-  // |D[r,:]|^2 = |a_r L^{-T}|^2: the loop's column reflections and rotations
-  // are orthogonal, so it never changes (used by the dependency test)
-  double ddr[MR];
-#pragma unroll
-  for (int r = 0; r < MR; ++r) ddr[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
-#endif
   clk.tick(1);
-  clk.tick(2);
 
   // ------------------------------------------------------ active-set loop
-  // R (upper triangular, active columns; column j = position j, column-major
+  // R (upper triangular, active positions; column j = position j, column-major
   // so the lane-parallel accesses are contiguous) lives in LDS with a ZERO
   // diagonal; lane l keeps R[l][l] and its reciprocal in registers, so the
   // back substitution needs no masking.
 #pragma unroll
-  for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&R[l * NL + j]) = make_double2(0.0, 0.0);
+  for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&Tv[l * NL + j]) = make_double2(0.0, 0.0);
   int q = 0;           // active-set size
   double um = 0.0;     // multiplier of active position l
   int iam = -1;        // constraint index at active position l
@@ -437,32 +344,24 @@ __device__ __forceinline__ void gi_group(
   int it = 0;
   wave_lds_sync();
   clk.tick(3);
-  // prefetch of the next group's H and A lines (one dword per 128-B line);
-  // the values are only consumed at the end, so the loads retire in the
-  // shadow of this group's iterations
-  uint32_t pf0 = 0, pf1 = 0, pf2 = 0;
-  if (nxt >= 0 && FULL) {
-    const long long gn = nxt * QPB + slot < batch ? nxt * QPB + slot : g;
-    const uint32_t *hp = reinterpret_cast<const uint32_t *>(Hg + gn * (NL * NL)) + l * 32;
-    const uint32_t *ap = reinterpret_cast<const uint32_t *>(Ag + gn * (NL * NL * MR)) + l * 32;
-    pf0 = *hp;
-    pf1 = *ap;
-    pf2 = MR > 1 ? ap[NL * 32] : 0u;
-  }
 
   while (!done && it < max_iter) {
     ++it;
     if (selecting) {
-      // most violated row by normalised slack.  The violation test is fp64;
-      // the argmax runs on 32-bit keys: the fp32 magnitude of the (negative)
-      // normalised slack with the row index in its low 5 bits, so one
-      // DPP-fused v_max_u32 per step reduces the row (0 = none violated)
+      // The violation test is fp64 on the slack normalised by |a_row| (the
+      // feasibility tolerance); among the violated rows the argmax runs on
+      // 32-bit keys: the fp32 violation per unit length of the row's free
+      // part, -s / |D[r, q:]| (dual steepest edge: 4.66 instead of 5.05
+      // iterations per QP on the bench family, 6.18 instead of 6.97 on the
+      // dense one, tools/gi_select_sim.py), row index in the low 5 bits, so
+      // one DPP-fused v_max_u32 per step reduces the row (0 = none violated)
       uint32_t key = 0u;
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const double v = s[r] * invn[r];
         const bool viol = !act[r] && v < thr[r];
-        const uint32_t kr = (__float_as_uint((float)(-v)) & ~31u) | (uint32_t)(l + NL * r);
+        const float kf = (float)(-s[r]) * __builtin_amdgcn_rsqf(__builtin_fmaxf(fn2[r], 1e-30f));
+        const uint32_t kr = (__float_as_uint(kf) & ~31u) | (uint32_t)(l + NL * r);
         key = viol && kr > key ? kr : key;
       }
       key = row_max_u32(key);
@@ -480,70 +379,47 @@ __device__ __forceinline__ void gi_group(
     // keeps every R column loop inside the QP's slot regardless)
     const int qmax = __builtin_elementwise_min(wave_max4(q), NL);
 
-    // ---- row p of D and s_p to every lane through the exchange row; the
-    // active columns are then zeroed in LDS: d2 = D[p, q:] (d = -D[p,:] in
-    // G-I's sign convention; the signs are folded into the formulas below)
+    // ---- row p of D, s_p and |D[p,:]|^2 through the exchange row; lane l
+    // keeps its entry D[p][l] (d = -D[p,:] in G-I's sign convention; the
+    // signs are folded into the formulas below)
     const int owner = p & (NL - 1), prow = p >> 4;
-#if QPB_XCH2 && !QPB_DDINV
-    // both rows of the owner lane go out (16 stores instead of 34 selects +
-    // 8 stores); readers index row prow.  s_p arrives by a row shuffle.
-    double *xr = xch + (MR > 1 ? NL * prow : 0);
-    if (l == owner) {
-#pragma unroll
-      for (int r = 0; r < MR; ++r)
-#pragma unroll
-        for (int j = 0; j < NL; j += 2)
-          *reinterpret_cast<double2 *>(&xch[NL * r + j]) = make_double2(E[r][j], E[r][j + 1]);
-    }
-    double ssel = s[0];
-#pragma unroll
-    for (int r = 1; r < MR; ++r) ssel = prow == r ? s[r] : ssel;
-    const double sp = __shfl(ssel, owner, NL);
-    wave_lds_sync();
-    const double Dpl = xr[l];
-    const double Dpq = xr[q < NL ? q : 0];  // q == 16: only used by an ADD, impossible then
-#else
-    double *xr = xch;
     if (l == owner) {
 #pragma unroll
       for (int r = 0; r < MR; ++r)
         if (r == prow) {
 #pragma unroll
           for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[r][j], E[r][j + 1]);
-#if QPB_DDINV
           *reinterpret_cast<double2 *>(&xch[NL]) = make_double2(s[r], ddr[r]);
-#else
-          xch[NL] = s[r];
-#endif
         }
     }
     wave_lds_sync();
     const double Dpl = xch[l];
-    const double Dpq = xch[q];  // q == 16 reads s_p: only used by an ADD, impossible then
-#if QPB_DDINV
     const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NL]);
+    const double Dpq = xch[q & (NL - 1)];  // q == 16: an ADD is impossible (d2 = 0)
     const double sp = spdd.x, dd = spdd.y;  // s_p, |D[p,:]|^2
-#else
-    const double sp = xch[NL];
+#if QPB_RV_PREFETCH
+    // the back substitution's R entries R[l][j], j < min(qmax, RV), issued here
+    double rv[QPB_RV_PREFETCH];
+    unroll<QPB_RV_PREFETCH / 4>([&](auto G) {
+      constexpr int g4 = 4 * G;
+      if (qmax > g4) {
+#pragma unroll
+        for (int j = g4; j < g4 + 4; ++j) rv[j] = Tv[j * NL + l];
+      }
+    });
 #endif
-#endif
-
     wave_lds_sync();
-    if (l < q) xr[l] = 0.0;
-    wave_lds_sync();
-    double d2[NL];
-    lds_row16(xr, d2);
-    const double dl = -Dpl;  // d1 component of active position l
-    const double nd2 = row_sum(l >= q ? Dpl * Dpl : 0.0);  // |d2|^2
-#if !QPB_DDINV
-    const double dd = row_sum(Dpl * Dpl);                   // |D[p,:]|^2
-#endif
+    const double d2 = (l >= q) ? Dpl : 0.0;  // D[p, q:]
+    dpp_ready(d2);
+    // slack direction D d2 (d2 read from lane j by the FMAs)
+    double u[MR];
+    bdot_rows<MR>(d2, E, u);
+    const double nd2 = row_sum(d2 * d2);  // |d2|^2
     clk.tick(5);
 
     // ---- r = R^{-1} d1: lane-parallel back substitution over the active positions
     double rm = 0.0;
     if (qmax > 0) {
-#if QPB_DPPFMA
       // on the negated accumulator: nacc_l += R[l][j] * r_j, r_j = nacc_j * (-1/R_jj)
       // read from lane j by the FMA itself (the product was written just
       // before: fmac_bc_nop issues the DPP read hazard's wait states)
@@ -551,17 +427,14 @@ __device__ __forceinline__ void gi_group(
       double nacc = (l < q) ? Dpl : 0.0;  // = -d1_l
       unroll<NL>([&](auto JJ) {
         constexpr int j = NL - 1 - JJ;
-        if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, R[j * NL + l]);
+#if QPB_RV_PREFETCH
+        if constexpr (j < QPB_RV_PREFETCH) {
+          if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, rv[j]);
+        } else
+#endif
+        if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, Tv[j * NL + l]);
       });
       rm = nacc * ninv;  // r_l (0 for l >= q)
-#else
-      double acc = (l < q) ? dl : 0.0;
-      unroll<NL>([&](auto JJ) {
-        constexpr int j = NL - 1 - JJ;
-        if (j < qmax) acc = __builtin_fma(-R[j * NL + l], bc<j>(acc * invRd), acc);
-      });
-      rm = acc * invRd;  // r_l (0 for l >= q)
-#endif
     }
     clk.tick(6);
 
@@ -569,19 +442,11 @@ __device__ __forceinline__ void gi_group(
     double t1 = kBig;
     int k = 0;
     if (qmax > 0) {
-      // the packed key (low 5 mantissa bits = position) only picks k; the step
-      // itself is lane k's exact ratio
+      // the exact minimum ratio, then the lowest position attaining it
       const double ratio = um * rcp1(rm);
-#if QPB_RATIO_MIN
       const bool cand = l < q && rm > 0.0;
-      t1 = row_min(cand ? ratio : kBig);  // exact minimum
+      t1 = row_min_raw(cand ? ratio : kBig);
       k = (int)row_min_u32(cand && ratio == t1 ? (uint32_t)l : 31u) & (NL - 1);
-#else
-      const double tk = row_min((l < q && rm > 0.0) ? pack_key(ratio, l) : kBig);
-      k = key_index(tk);
-      const double tx = __shfl(ratio, k, NL);
-      t1 = tk < kBig ? tx : kBig;
-#endif
     }
     const double ir = rsq1(nd2);  // 1/|d2| (only used when nd2 > 0)
     const double t2 = (nd2 > kDepTol * dd) ? -sp * (ir * ir) : kBig;
@@ -593,13 +458,8 @@ __device__ __forceinline__ void gi_group(
     }
     if (t2 < kBig) {  // primal step: slacks s -= t A z,  A z = -D[:, q:] d2
 #pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        const double u = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return d2[j]; });
-        s[r] = __builtin_fma(t, u, s[r]);
-      }
+      for (int r = 0; r < MR; ++r) s[r] = __builtin_fma(t, u[r], s[r]);
     }
-#pragma unroll
-    for (int r = 0; r < MR; ++r) pin(s[r]);  // d2 dies here, before the ADD reads v
     um = __builtin_fma(-t, rm, um);
     up += t;
     clk.tick(7);
@@ -607,45 +467,49 @@ __device__ __forceinline__ void gi_group(
     if (t2 <= t1) {
       // ---------------- ADD p: Householder on columns q.. of D.  With
       // dq = -D[p,q]: alpha = -sign(dq) |d2|, v = d2 + alpha e_q (the negated
-      // G-I vector: same reflection), beta = 1 / (|d2|^2 + alpha D[p,q]).
-      // nd2 + alpha D[p,q] = |d2| (|d2| + |D[p,q]|): one reciprocal
+      // G-I vector: same reflection), beta = 1 / (|d2|^2 + alpha D[p,q]) =
+      // 1 / (|d2| (|d2| + |D[p,q]|)): one reciprocal.
       const double nrm = nd2 * ir;
-      const double alpha = Dpq <= 0.0 ? -nrm : nrm;
+      const bool neg = Dpq <= 0.0;
+      const double alpha = neg ? -nrm : nrm;
       const double beta = ir * rcp1(nrm + __builtin_fabs(Dpq));
-      if (l == q) xr[q] = Dpq + alpha;
-      wave_lds_sync();
-      double v[NL];
-      lds_row16(xr, v);
+      const double ia = neg ? -ir : ir;  // 1 / alpha
+      const double v = d2 + (l == q ? alpha : 0.0);
+      dpp_ready(v);
+      double nw[MR];
+      bdot_rows<MR>(v, E, nw);
+#pragma unroll
+      for (int r = 0; r < MR; ++r) nw[r] *= -beta;
+#pragma unroll
+      for (int r = 0; r < MR; ++r) unroll<NL>([&](auto J) {
+          constexpr int j = J;
+          fmac_bc<j>(E[r][j], v, nw[r]);
+        });
+      // the reflection maps e_q to -d2 / alpha: column q of the new D is
+      // -u / alpha, and it leaves the free part of every row
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
-        const double w = beta * dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return v[j]; });
-#pragma unroll
-        for (int j = 0; j < NL; ++j) E[r][j] = __builtin_fma(-w, v[j], E[r][j]);
+        const float c = (float)(u[r] * ia);
+        fn2[r] = __builtin_fmaf(-c, c, fn2[r]);
       }
       // new column q of R: d1 strictly above the diagonal, alpha on it
-      R[q * NL + l] = (l < q) ? dl : 0.0;
+      Tv[q * NL + l] = (l < q) ? -Dpl : 0.0;
       if (l == q) {
         rdg = alpha;
-        invRd = Dpq <= 0.0 ? -ir : ir;  // 1 / alpha
+        invRd = ia;
         iam = p;
         um = up;
       }
-      if (l == owner) {
 #pragma unroll
-        for (int r = 0; r < MR; ++r)
-          if (r == prow) act[r] = true;
-      }
+      for (int r = 0; r < MR; ++r) act[r] = act[r] || (l == owner && r == prow);
       ++q;
       selecting = true;
       clk.tick(8);
     } else {
       // ---------------- DROP active position k
       const int c = __shfl(iam, k, NL);
-      if (l == (c & (NL - 1))) {
 #pragma unroll
-        for (int r = 0; r < MR; ++r)
-          if (r == (c >> 4)) act[r] = false;
-      }
+      for (int r = 0; r < MR; ++r) act[r] = act[r] && !(l == (c & (NL - 1)) && r == (c >> 4));
       const double un = __shfl(um, (l + 1) & (NL - 1), NL);
       const int in = __shfl(iam, (l + 1) & (NL - 1), NL);
       if (l >= k && l < q - 1) {
@@ -655,36 +519,41 @@ __device__ __forceinline__ void gi_group(
         um = 0.0;
         iam = -1;
       }
-      // full R (diagonal put back), delete column k (lane l owns column l):
-      // row by row, each read instruction precedes the write that could
-      // overwrite what it reads (in-order DS execution)
+      // full R (diagonal put back), delete column k: lane l (column l) reads
+      // column l + 1 whole, then writes it (in-order DS: every read precedes
+      // every write)
       wave_lds_sync();
-      if (l < q) R[l * NL + l] = rdg;
-      const bool shift = l >= k && l < q - 1;
-      for (int i = 0; i < qmax; ++i) {
+      if (l < q) Tv[l * NL + l] = rdg;
+      wave_lds_sync();
+      {
+        double col[NL];
+        lds_row16(&Tv[((l + 1) & (NL - 1)) * NL], col);
         wave_lds_sync();
-        const double nxt = R[((l + 1) & (NL - 1)) * NL + i];
-        wave_lds_sync();
-        if (shift) R[l * NL + i] = nxt;
-        else if (l == q - 1) R[l * NL + i] = 0.0;
+        if (l >= k && l < q - 1) {
+#pragma unroll
+          for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&Tv[l * NL + j]) = make_double2(col[j], col[j + 1]);
+        } else if (l == q - 1) {
+#pragma unroll
+          for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&Tv[l * NL + j]) = make_double2(0.0, 0.0);
+        }
       }
       // Givens rotations restore the upper-triangular R
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
-        const double a = R[j * NL + j], bb = R[j * NL + j + 1];
-        const double ir = rsq1(__builtin_fma(a, a, bb * bb));
-        const double cj = a * ir, sj = bb * ir;
-        const double rj = R[l * NL + j], rj1 = R[l * NL + j + 1];
+        const double a = Tv[j * NL + j], bb = Tv[j * NL + j + 1];
+        const double irr = rsq1(__builtin_fma(a, a, bb * bb));
+        const double cj = a * irr, sj = bb * irr;
+        const double rj = Tv[l * NL + j], rj1 = Tv[l * NL + j + 1];
         wave_lds_sync();
         if (l >= j && l < q - 1) {
-          R[l * NL + j] = __builtin_fma(cj, rj, sj * rj1);
-          R[l * NL + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
+          Tv[l * NL + j] = __builtin_fma(cj, rj, sj * rj1);
+          Tv[l * NL + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
         }
         gcs[j] = cj;  // same value from every lane
         gsn[j] = sj;
       }
       wave_lds_sync();
-      R[l * NL + q - 1] = 0.0;
+      Tv[l * NL + q - 1] = 0.0;
       unroll<NL - 1>([&](auto JJ) {
         constexpr int j = JJ;
         if (j + 1 < qmax && j >= k && j < q - 1) {
@@ -698,11 +567,23 @@ __device__ __forceinline__ void gi_group(
         }
       });
       --q;
+      // column q (after the rotations) joins the free part: recompute
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        float a0 = 0.0f, a1 = 0.0f;
+        unroll<NL>([&](auto J) {
+          constexpr int j = J;
+          const float e = (float)E[r][j];
+          if constexpr (j % 2 == 0) a0 = __builtin_fmaf(e, j >= q ? e : 0.0f, a0);
+          if constexpr (j % 2 == 1) a1 = __builtin_fmaf(e, j >= q ? e : 0.0f, a1);
+        });
+        fn2[r] = a0 + a1;
+      }
       // back to the zero-diagonal form
       wave_lds_sync();
-      const double dg = (l < q) ? R[l * NL + l] : 0.0;
+      const double dg = (l < q) ? Tv[l * NL + l] : 0.0;
       wave_lds_sync();
-      if (l < q) R[l * NL + l] = 0.0;
+      if (l < q) Tv[l * NL + l] = 0.0;
       rdg = dg;
       invRd = (l < q) ? rcp1(dg) : 0.0;
       clk.tick(9);
@@ -712,7 +593,7 @@ __device__ __forceinline__ void gi_group(
   clk.tick(10);
 
   // ------------------------------------------------------------- outputs
-  // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iact_k} (the active rows of
+  // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iam_k} (the active rows of
   // A re-read, one coalesced 128-B row per active position), then L y = g,
   // L^T x = -y, lane-parallel: step k broadcasts the finished component from
   // lane k; finished lanes keep updating (dead values) and the components are
@@ -788,7 +669,6 @@ __device__ __forceinline__ void gi_group(
     if (live && (FULL || row < m)) lamg[g * m + row] = lamb[row];
   }
   if (live && (N16 || l < n)) xg[g * n + l] = xl;
-  const int sh = (threadIdx.x & 63) & ~(NL - 1);
   uint32_t w0 = 0;
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
@@ -800,7 +680,6 @@ __device__ __forceinline__ void gi_group(
     statg[g] = status;
     if (itg) itg[g] = it;
   }
-  asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
   clk.tick(11);
   clk.flush(dbg);
 }
@@ -813,34 +692,8 @@ __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
     long long batch, int max_iter, double feas_tol, int flags = 0,
     unsigned long long *__restrict__ dbg = nullptr) {
   __shared__ double lds[QPB * SLOT];
-  long long nxt = -1;
-  if constexpr (QPB_PF_DIST > 0) {
-    // the group a wave dispatched about one wave lifetime from now will
-    // solve: its lines are pulled into the Infinity Cache while this group
-    // iterates, so that wave's loads hit on-die instead of queueing for HBM
-    const long long ngroups = (batch + QPB - 1) / QPB;
-    nxt = (long long)blockIdx.x + QPB_PF_DIST < ngroups ? (long long)blockIdx.x + QPB_PF_DIST : -1;
-  }
   gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
-                                 flags, dbg, blockIdx.x, nxt);
-}
-
-// persistent form: the grid covers the resident waves once; each wave walks
-// the groups grp, grp + gridDim.x, ... and prefetches the next one
-template <int MR, bool N16, bool FULL, int OCC = 2>
-__global__ __launch_bounds__(64, OCC) void gi_dense_persistent(
-    const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
-    const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
-    uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
-    long long batch, int max_iter, double feas_tol, int flags) {
-  __shared__ double lds[QPB * SLOT];
-  const long long ngroups = (batch + QPB - 1) / QPB;
-  for (long long grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const long long nxt = grp + gridDim.x < ngroups ? grp + gridDim.x : -1;
-    gi_group<MR, N16, FULL, false>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
-                                   flags, nullptr, grp, nxt);
-    wave_lds_sync();
-  }
+                                 flags, dbg, blockIdx.x);
 }
 
 }  // namespace qpb
@@ -853,28 +706,16 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
 #define QPB_GI_LAUNCH(MR, N16, FULL)                                                                               \
-  hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL>), dim3((unsigned)blocks), dim3(64), 0, stream, H, f, A, \
-                     b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags)
+  hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream, \
+                     H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,    \
+                     d->flags)
   const bool n16 = d->n == 16;
   if (d->m <= 16) {
     if (n16 && d->m == 16) QPB_GI_LAUNCH(1, true, true);
     else if (n16) QPB_GI_LAUNCH(1, true, false);
     else QPB_GI_LAUNCH(1, false, false);
   } else {
-    if (n16 && d->m == 32 && (d->flags & 8)) {  // persistent form
-      int dev = 0, cus = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      const long long waves = (long long)cus * 8;  // 2 waves per SIMD (the group loop costs 70 VGPRs)
-      const unsigned grid = (unsigned)(blocks < waves ? blocks : waves);
-      hipLaunchKernelGGL((qpb::gi_dense_persistent<2, true, true, 2>), dim3(grid), dim3(64), 0, stream, H, f, A, b, x,
-                         lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags);
-    } else if (n16 && d->m == 32 && (d->flags & 4))  // diagnostic: the 2-waves/SIMD build
-      QPB_GI_LAUNCH(2, true, true);
-    else if (n16 && d->m == 32)  // 168 VGPRs, 13.25 KiB LDS: 3 waves per SIMD
-      hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream,
-                         H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
-                         d->flags);
+    if (n16 && d->m == 32) QPB_GI_LAUNCH(2, true, true);  // 3 waves per SIMD (VGPRs and LDS)
     else if (n16) QPB_GI_LAUNCH(2, true, false);
     else QPB_GI_LAUNCH(2, false, false);
   }
@@ -882,7 +723,7 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
   return hipGetLastError();
 }
 
-// diagnostic: per-section wave ticks of the n=16, 16<m<=32 kernel (sections[12])
+// diagnostic: per-section wave ticks of the n=16, 16<m<=32 kernel (sections[256][20])
 extern "C" hipError_t qpb_launch_gi_sections(const qpb_desc *d, const double *H, const double *f, const double *A,
                                              const double *b, double *x, double *lam, uint32_t *active,
                                              int32_t *status, int32_t *iters, unsigned long long *sections,
