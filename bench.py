@@ -67,10 +67,18 @@ def baseline_config(n: int, total: int, world: int) -> str:
     return "not a BASELINE config"
 
 
+def kernel_revisions(library: str) -> set:
+    """The per-kernel revision tokens of qpb_version(): "qpb X (gfx950; gi_dense
+    v10: ...; gi_box v1: ...)" -> {"gi_dense v10", "gi_box v1", ...}."""
+    inner = library.split("(", 1)[1].rsplit(")", 1)[0] if "(" in library else library
+    return {part.split(":", 1)[0].strip() for part in inner.split(";") if ":" in part}
+
+
 def pmc_traffic(n: int, m: int, B: int, family: str, library: str):
     """HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE,
-    WRITE_SIZE; gfx950-corrected, tools/summarize_profile.py) for this exact
-    kernel configuration, from the committed profiles/pmc_traffic.json, or None."""
+    WRITE_SIZE; gfx950-corrected, tools/summarize_profile.py) and the VALU
+    instruction classes per wave, for this exact kernel configuration and
+    revision, from the committed profiles/pmc_traffic.json, or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         t = json.load(open(path))
@@ -80,26 +88,39 @@ def pmc_traffic(n: int, m: int, B: int, family: str, library: str):
     if (c.get("n"), c.get("m"), c.get("batch_per_gpu"), c.get("family")) != (n, m, B, family):
         return None
     rev = t.get("kernel_rev")
-    if not rev or rev not in library:  # measured on another revision of the hot kernel
+    if not rev or rev not in kernel_revisions(library):  # measured on another revision of the hot kernel
         return None
     return {"bytes": t["hbm_bytes_per_launch"], "source": t.get("source", path),
-            "valu_insts_per_wave": t.get("valu_insts_per_wave"), "valu_source": t.get("valu_source")}
+            "valu_classes": t.get("valu_classes"), "valu_source": t.get("valu_source")}
 
 
-VALU_CYCLES = 4  # one wave64 VALU instruction on a 16-lane SIMD (fp64 FMA at the 78.6 TF/s vector rate)
+# Issue cost of one wave64 instruction per SIMD, by class (cycles at 2.4 GHz,
+# many waves per SIMD: tools/probe/valu_probe.hip, profiles/r03/valu_probe_r03.jsonl).
+# fp64 add has no probe of its own and is charged as mul; the 32-bit classes
+# (integer, conversions, selects, DPP moves, the rest of SQ_INSTS_VALU) at the
+# v_fma_f32 rate.
+VALU_COST = {"FMA_F64": 5.24, "MUL_F64": 5.47, "ADD_F64": 5.47, "TRANS_F64": 17.23, "B32": 3.07}
 SIMDS, CLOCK_GHZ = 1024, 2.4  # MI355X: 256 CUs x 4 SIMDs, peak engine clock
 
 
 def valu_ceiling(traffic, waves: int, kern_ms: float):
-    """The kernel's issue-rate bound: the PMC-measured VALU instructions per
-    wave (SQ_INSTS_VALU / SQ_WAVES, committed with the traffic numbers) issued
-    back to back on every SIMD at the peak clock, against the measured time."""
-    if not traffic or not traffic.get("valu_insts_per_wave"):
+    """The kernel's issue-rate bound: every VALU instruction class of the
+    committed PMC pass (SQ_INSTS_VALU_FMA_F64 / _MUL_F64 / _ADD_F64 /
+    _TRANS_F64 per wave; the rest of SQ_INSTS_VALU as 32-bit) charged its
+    measured issue cost, issued back to back on every SIMD at the peak clock,
+    against the measured kernel time."""
+    cls = (traffic or {}).get("valu_classes")
+    if not cls or not cls.get("VALU"):
         return None
-    ms = traffic["valu_insts_per_wave"] * VALU_CYCLES * waves / SIMDS / (CLOCK_GHZ * 1e9) * 1e3
-    return {"valu_insts_per_wave": traffic["valu_insts_per_wave"], "cycles_per_inst": VALU_CYCLES,
+    f64 = {k: cls.get(k, 0.0) for k in ("FMA_F64", "MUL_F64", "ADD_F64", "TRANS_F64")}
+    b32 = max(0.0, cls["VALU"] - sum(f64.values()))
+    cycles = sum(VALU_COST[k] * v for k, v in f64.items()) + VALU_COST["B32"] * b32
+    ms = cycles * waves / SIMDS / (CLOCK_GHZ * 1e9) * 1e3
+    return {"valu_insts_per_wave": cls["VALU"], "classes_per_wave": dict(f64, B32=b32),
+            "cycles_per_class": VALU_COST, "issue_cycles_per_wave": cycles,
             "ceiling_ms": ms, "kernel_ms": kern_ms, "frac": ms / kern_ms, "source": traffic.get("valu_source"),
-            "note": "time if every SIMD issued one VALU instruction every 4 cycles at 2.4 GHz with no stall"}
+            "note": "time if every SIMD issued the wave's instructions back to back at their measured costs "
+                    "(2.4 GHz, no stall)"}
 
 
 # --------------------------------------------------------------------------- CPU share
@@ -260,6 +281,21 @@ def main():
     import qpb
     from qpb.dist import gather_results, max_over_ranks, shard
 
+    dist_info = None
+    if world > 1:
+        # which GPUs the ranks actually drive (RCCL must see N distinct devices)
+        import torch.distributed as dist
+        props = torch.cuda.get_device_properties(device)
+        mine = {"rank": rank, "local_rank": local, "device": device.index,
+                "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", ""))}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        ids = [(r["pci_bus_id"], r["uuid"]) for r in ranks]
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": ranks,
+                     "distinct_devices": len(set(ids)) == world}
+        if dist_info["backend"] == "nccl" and not dist_info["distinct_devices"]:
+            raise SystemExit(f"bench.py: RCCL ranks share a GPU: {ranks}")
+
     n, m = args.n, 2 * args.n
     if args.batch:
         start, B = rank * args.batch, args.batch
@@ -393,6 +429,7 @@ def main():
             "box_fast_path": box,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
             "gather_ms": gather_ms,
+            "distributed": dist_info,
             "library": qpb.version(),
         }
         print(json.dumps(line), flush=True)

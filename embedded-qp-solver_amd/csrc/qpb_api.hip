@@ -27,9 +27,6 @@ extern "C" hipError_t qpb_launch_gi_wave(const qpb_desc *d, const double *H, con
 extern "C" hipError_t qpb_launch_gi_mixed(const qpb_desc *d, const double *H, const double *f, const double *A,
                                           const double *b, double *x, double *lam, uint32_t *active,
                                           int32_t *status, int32_t *iters, hipStream_t stream);
-extern "C" hipError_t qpb_launch_gi_block(const qpb_desc *d, const double *H, const double *f, const double *A,
-                                          const double *b, double *x, double *lam, uint32_t *active,
-                                          int32_t *status, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
                                          const double *b, double *x, double *lam, uint32_t *active,
                                          int32_t *status, int32_t *iters, unsigned long long *sections,
@@ -92,7 +89,7 @@ static int check_device(void) {
 static long long chunk_qps(int n, int m) {
   if (n <= 16 && m <= 32) return 1LL << 27;  // 16 lanes per QP
   if (n <= 32 && m <= 64) return 1LL << 25;  // 64 lanes per QP
-  return 1LL << 21;                          // 1024 lanes per QP
+  return 1LL << 21;                          // n <= 128: one workgroup per CU walks the QPs (bounded chunks)
 }
 
 static int check_desc(const qpb_desc *d) {
@@ -130,12 +127,10 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
     hipError_t e;
     if (d->n <= 16 && d->m <= 32)
       e = qpb_launch_gi(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
-    else if (d->n <= 32 && d->m <= 64 && (d->flags & QPB_FLAG_MIXED))
+    else if (d->n > 16 && d->n <= 32 && d->m <= 64 && (d->flags & QPB_FLAG_MIXED))
       e = qpb_launch_gi_mixed(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
     else if (d->n <= 32 && d->m <= 64)
       e = qpb_launch_gi_wave(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
-    else if (d->flags & QPB_FLAG_DIAG_BLOCK)
-      e = qpb_launch_gi_block(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
     else
       e = qpb_launch_gi_gram(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, nullptr, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "qpb_solve launch");
@@ -389,4 +384,4 @@ extern "C" const char *qpb_last_error(void) { return g_err; }
 
 // the hot kernel revision is part of the string: profiles/pmc_traffic.json is
 // only trusted for the revision it was measured on (bench.py)
-extern "C" const char *qpb_version(void) { return "qpb 0.7 (gfx950; gi_dense v8.1: DPP-fused fmac sweep, in-sweep slacks, exact ratio step, one-trip loads and x gather, fp32-key select, 3 waves/SIMD; gi_box v1: lb <= x <= ub, A implicit; gi_wave v3: one-trip A gather for x, 32-bit key select, split setup sweep, 3 waves/SIMD; gi_gram v3 n<=128 on fp64 MFMA, broadcast row products, one-trip loads; ref v2: parallel independent sums)"; }
+extern "C" const char *qpb_version(void) { return "qpb 0.8 (gfx950; gi_dense v10: dual steepest-edge select -s/|D[r,q:]|, DPP-fused slack and Householder products, exact ratio step, one-trip loads and x gather, 3 waves/SIMD; gi_box v1: lb <= x <= ub, A implicit; gi_wave v3: one-trip A gather for x, 32-bit key select, split setup sweep, 3 waves/SIMD; gi_gram v3 n<=128 on fp64 MFMA, broadcast row products, one-trip loads, cached workspace; ref v3: n <= 128, LU in a global workspace above 64)"; }

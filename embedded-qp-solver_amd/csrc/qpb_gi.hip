@@ -62,18 +62,22 @@ constexpr int RS = 18;  // row stride (doubles) of the input transposes: conflic
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
 constexpr int L_SIZE = lrow(NL);  // 136
 
-// LDS slot of one QP: 424 doubles = 3,392 B, 13,568 B per wave -> 12 waves
+// LDS slot of one QP: 426 doubles = 3,408 B, 13,632 B per wave -> 12 waves
 // per CU (3 per SIMD, matching the VGPR budget)
 constexpr int OFF_L = 0;                  // L (136)
 constexpr int OFF_T = L_SIZE;             // R, column-major 16 x 16: R[i][j] at j*16 + i
-constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: exchange row d (16), s_p, |d|^2; Givens cos / sin
-                                          // (16 + 16); y / x capture; lambda scatter
-constexpr int SLOT = OFF_XCH + 32;        // 424
+constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: exchange rows (MR x 16), s_p, |d|^2; Givens
+                                          // cos / sin (16 + 16); y / x capture; lambda scatter
+constexpr int SLOT = OFF_XCH + 34;        // 426 (4 x 426 x 8 B = 13,632 B per wave: 12 waves per CU)
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
+#ifndef QPB_XCH_ALL
+#define QPB_XCH_ALL 0  // 1: the owner writes all its rows, no VALU selects (+2.3 % box, +3.0 % dense: profiles/r03/ab/ab_v12*.json)
+#endif
 #ifndef QPB_RV_PREFETCH
 #define QPB_RV_PREFETCH 0  // R entries of the back substitution read ahead (multiple of 4, <= 16): 8 spills (+21 %)
 #endif
 static_assert(SLOT % 2 == 0 && OFF_T % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
+static_assert(4 * SLOT * 8 <= 160 * 1024 / 12, "12 waves (3 per SIMD) per CU by LDS");
 static_assert(NL * RS <= SLOT - OFF_T, "input transposes are staged in T + xch");
 
 // sum_{j<N} x(j) y(j) with 2 independent accumulators
@@ -163,7 +167,8 @@ __device__ __forceinline__ void gi_group(
   const double *bq = m > 0 ? bg + gi * (long long)m : Hq;
   double Lr[NL];  // row l of H, becomes row l of L
   double E[MR][NL];
-  double s[MR], invn[MR], bl[MR], thr[MR], ddr[MR];
+  double s[MR], bl[MR], thr[MR];
+  float ddr[MR];  // |D[r,:]|^2 (the dependency test's scale)
   float fn2[MR];  // |D[r, q:]|^2, the free part of the row (scale of the selection key)
   bool act[MR];
   bool infeasible_row = false;
@@ -242,9 +247,9 @@ __device__ __forceinline__ void gi_group(
     const bool ok = FULL || row < m;
     const double nrm2 = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
     bl[r] = ok ? bv[r] : 0.0;
-    invn[r] = nrm2 > 0.0 ? rsq1(nrm2) : 0.0;
-    // violation threshold of the normalised slack (-inf: zero row, never selected)
-    thr[r] = nrm2 > 0.0 ? -feas_tol * (1.0 + __builtin_fabs(bl[r]) * invn[r]) : -kInf;
+    // violation threshold of the slack: s / |a| < -tol (1 + |b| / |a|), i.e.
+    // s < -tol (|a| + |b|)  (-inf: zero row, never selected)
+    thr[r] = nrm2 > 0.0 ? -feas_tol * (nrm2 * rsq1(nrm2) + __builtin_fabs(bl[r])) : -kInf;
     // a zero row is the constant constraint 0 <= b
     infeasible_row = infeasible_row || (ok && nrm2 == 0.0 && bl[r] < -feas_tol * (1.0 + __builtin_fabs(bl[r])));
     act[r] = false;
@@ -312,22 +317,21 @@ __device__ __forceinline__ void gi_group(
   // never changes (the dependency test's scale)
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
-    ddr[r] = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
-    fn2[r] = (float)ddr[r];
+    ddr[r] = (float)dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
+    fn2[r] = ddr[r];
   }
   clk.tick(1);
 
   // ------------------------------------------------------ active-set loop
   // R (upper triangular, active positions; column j = position j, column-major
   // so the lane-parallel accesses are contiguous) lives in LDS with a ZERO
-  // diagonal; lane l keeps R[l][l] and its reciprocal in registers, so the
-  // back substitution needs no masking.
+  // diagonal; lane l keeps 1 / R[l][l] in a register, so the back
+  // substitution needs no masking.
 #pragma unroll
   for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&Tv[l * NL + j]) = make_double2(0.0, 0.0);
   int q = 0;           // active-set size
   double um = 0.0;     // multiplier of active position l
   int iam = -1;        // constraint index at active position l
-  double rdg = 0.0;    // R[l][l]
   double invRd = 0.0;  // 1 / R[l][l]
   int status;
   bool done;
@@ -358,9 +362,8 @@ __device__ __forceinline__ void gi_group(
       uint32_t key = 0u;
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
-        const double v = s[r] * invn[r];
-        const bool viol = !act[r] && v < thr[r];
-        const float kf = (float)(-s[r]) * __builtin_amdgcn_rsqf(__builtin_fmaxf(fn2[r], 1e-30f));
+        const bool viol = !act[r] && s[r] < thr[r];
+        const float kf = (float)(-s[r]) * __builtin_amdgcn_rsqf(fn2[r]);  // fn2 >= 0 (clamped where it shrinks)
         const uint32_t kr = (__float_as_uint(kf) & ~31u) | (uint32_t)(l + NL * r);
         key = viol && kr > key ? kr : key;
       }
@@ -383,19 +386,43 @@ __device__ __forceinline__ void gi_group(
     // keeps its entry D[p][l] (d = -D[p,:] in G-I's sign convention; the
     // signs are folded into the formulas below)
     const int owner = p & (NL - 1), prow = p >> 4;
+#if QPB_XCH_ALL
+    // the owner lane writes all its MR rows (MR x 8 stores, no selects of the
+    // row on the VALU); readers index row prow
+    if (l == owner) {
+#pragma unroll
+      for (int r = 0; r < MR; ++r)
+#pragma unroll
+        for (int j = 0; j < NL; j += 2)
+          *reinterpret_cast<double2 *>(&xch[NL * r + j]) = make_double2(E[r][j], E[r][j + 1]);
+      double sr = s[0], dr = ddr[0];
+#pragma unroll
+      for (int r = 1; r < MR; ++r) {
+        sr = prow == r ? s[r] : sr;
+        dr = prow == r ? ddr[r] : dr;
+      }
+      *reinterpret_cast<double2 *>(&xch[NL * MR]) = make_double2(sr, dr);
+    }
+    wave_lds_sync();
+    const double *xr = xch + (MR > 1 ? NL * prow : 0);
+    const double Dpl = xr[l];
+    const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NL * MR]);
+    const double Dpq = xr[q & (NL - 1)];  // q == 16: an ADD is impossible (d2 = 0)
+#else
     if (l == owner) {
 #pragma unroll
       for (int r = 0; r < MR; ++r)
         if (r == prow) {
 #pragma unroll
           for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[r][j], E[r][j + 1]);
-          *reinterpret_cast<double2 *>(&xch[NL]) = make_double2(s[r], ddr[r]);
+          *reinterpret_cast<double2 *>(&xch[NL]) = make_double2(s[r], (double)ddr[r]);
         }
     }
     wave_lds_sync();
     const double Dpl = xch[l];
     const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NL]);
     const double Dpq = xch[q & (NL - 1)];  // q == 16: an ADD is impossible (d2 = 0)
+#endif
     const double sp = spdd.x, dd = spdd.y;  // s_p, |D[p,:]|^2
 #if QPB_RV_PREFETCH
     // the back substitution's R entries R[l][j], j < min(qmax, RV), issued here
@@ -490,12 +517,11 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const float c = (float)(u[r] * ia);
-        fn2[r] = __builtin_fmaf(-c, c, fn2[r]);
+        fn2[r] = __builtin_fmaxf(__builtin_fmaf(-c, c, fn2[r]), 0.0f);
       }
       // new column q of R: d1 strictly above the diagonal, alpha on it
       Tv[q * NL + l] = (l < q) ? -Dpl : 0.0;
       if (l == q) {
-        rdg = alpha;
         invRd = ia;
         iam = p;
         um = up;
@@ -523,7 +549,7 @@ __device__ __forceinline__ void gi_group(
       // column l + 1 whole, then writes it (in-order DS: every read precedes
       // every write)
       wave_lds_sync();
-      if (l < q) Tv[l * NL + l] = rdg;
+      if (l < q) Tv[l * NL + l] = rcp1(invRd);  // R[l][l] (alpha when it was added)
       wave_lds_sync();
       {
         double col[NL];
@@ -584,7 +610,6 @@ __device__ __forceinline__ void gi_group(
       const double dg = (l < q) ? Tv[l * NL + l] : 0.0;
       wave_lds_sync();
       if (l < q) Tv[l * NL + l] = 0.0;
-      rdg = dg;
       invRd = (l < q) ? rcp1(dg) : 0.0;
       clk.tick(9);
     }

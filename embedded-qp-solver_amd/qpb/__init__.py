@@ -41,9 +41,8 @@ ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_DEVICE = -1, -2, -3, -4
 REF_NEWTON, REF_ADMM, REF_GD = 1, 2, 3
 MAX_N, MAX_M = 128, 256
 # qpb_desc.flags (include/qpb.h)
-FLAG_DIAG_L2, FLAG_DIAG_OCC2, FLAG_DIAG_PERSISTENT, FLAG_DIAG_MALL = 1, 4, 8, 16
+FLAG_DIAG_L2, FLAG_DIAG_MALL = 1, 16
 FLAG_MIXED, FLAG_DIAG_NO_REDO = 32, 64
-FLAG_DIAG_BLOCK = 128  # n <= 128 class: the round-1 kernel (qpb_gi_block.hip)
 STATUS_REDO = 100  # internal: a QP the mixed kernel leaves to the fp64 re-solve (FLAG_DIAG_NO_REDO only)
 
 

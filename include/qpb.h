@@ -52,12 +52,14 @@
 extern "C" {
 #endif
 
+/* qpb_version() reports "qpb MAJOR.MINOR (...)" */
 #define QPB_VERSION_MAJOR 0
-#define QPB_VERSION_MINOR 2
+#define QPB_VERSION_MINOR 8
 
 /* limits of this build's kernels: n <= 16, m <= 32 one QP per 16-lane DPP
  * row (qpb_gi.hip); n <= 32, m <= 64 one QP per wavefront (qpb_gi_wave.hip);
- * n <= 128, m <= 256 one QP per 1024-thread workgroup (qpb_gi_gram.hip) */
+ * n <= 128, m <= 256 one QP per 512-thread workgroup, one workgroup per CU
+ * walking the batch (qpb_gi_gram.hip) */
 #define QPB_MAX_N 128
 #define QPB_MAX_M 256
 
@@ -80,11 +82,8 @@ typedef enum qpb_error {
 /* diagnostic flag: every QP k reads the inputs of QP (k mod 512) -- kernel
  * time without HBM latency (outputs are still written for every k) */
 #define QPB_FLAG_DIAG_L2 1
-/* diagnostic flag: n = 16, m = 32 solved by the 2-waves-per-SIMD build */
-#define QPB_FLAG_DIAG_OCC2 4
-/* diagnostic flag: n = 16, m = 32 by the persistent launch (grid = resident
- * waves, each walks several 4-QP groups and prefetches the next one) */
-#define QPB_FLAG_DIAG_PERSISTENT 8
+/* flag values 4 and 8 (round-2 diagnostic builds of the n <= 16 kernel) are
+ * retired: accepted and ignored */
 /* diagnostic flag (n <= 16): every QP k reads the inputs of QP (k mod 16384),
  * a 107 MB working set that stays Infinity-Cache resident across launches */
 #define QPB_FLAG_DIAG_MALL 16
@@ -101,10 +100,7 @@ typedef enum qpb_error {
  * would be re-solved keep status 100 (measures the re-solve fraction) */
 #define QPB_FLAG_DIAG_NO_REDO 64
 
-/* diagonal flag (32 < n <= 128 or 64 < m <= 256): the round-1 one-QP-per-
- * workgroup kernel (qpb_gi_block.hip, G-I on a register-resident rotating D)
- * instead of the Gram-form kernel (qpb_gi_gram.hip) -- kept for A/B runs */
-#define QPB_FLAG_DIAG_BLOCK 128
+/* flag value 128 (the round-1 n <= 128 kernel) is retired: accepted and ignored */
 
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */

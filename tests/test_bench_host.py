@@ -37,24 +37,33 @@ def test_baseline_config_names(bench):
 def test_pmc_traffic_is_keyed_by_kernel_revision(bench):
     t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     c = t["config"]
-    lib_ok = "qpb x.y (gfx950; " + t["kernel_rev"] + ": ...)"
+    lib_ok = "qpb x.y (gfx950; " + t["kernel_rev"] + ": desc, more; gi_box v1: ...)"
     got = bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], c["family"], lib_ok)
     assert got is not None and got["bytes"] == t["hbm_bytes_per_launch"]
-    assert got["valu_insts_per_wave"] == t["valu_insts_per_wave"]
+    assert got["valu_classes"] == t["valu_classes"]
     # another revision of the hot kernel, or another configuration: no number
     assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], c["family"], "qpb (gi_dense v0)") is None
+    # a revision that merely extends the committed one's name is another revision
+    longer = "qpb x.y (gfx950; " + t["kernel_rev"] + ".1: desc)"
+    assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], c["family"], longer) is None
+    assert bench.kernel_revisions(lib_ok) == {t["kernel_rev"], "gi_box v1"}
     assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"] // 2, c["family"], lib_ok) is None
     assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], "dense", lib_ok) is None
 
 
 def test_valu_ceiling(bench):
     assert bench.valu_ceiling(None, 1, 1.0) is None
-    t = {"valu_insts_per_wave": 3000.0, "valu_source": "x"}
+    t = {"valu_classes": {"VALU": 3000.0, "FMA_F64": 1000.0, "MUL_F64": 300.0, "ADD_F64": 100.0,
+                          "TRANS_F64": 40.0}, "valu_source": "x"}
     waves = 1 << 18  # 1 M QPs, four per wave
     v = bench.valu_ceiling(t, waves, 2.0)
-    # 3000 instructions x 4 cycles x 256 waves per SIMD at 2.4 GHz
-    assert v["ceiling_ms"] == pytest.approx(3000 * 4 * 256 / 2.4e9 * 1e3)
+    c = bench.VALU_COST
+    cyc = 1000 * c["FMA_F64"] + 300 * c["MUL_F64"] + 100 * c["ADD_F64"] + 40 * c["TRANS_F64"] + 1560 * c["B32"]
+    # every class at its measured cost, 256 waves per SIMD at 2.4 GHz
+    assert v["issue_cycles_per_wave"] == pytest.approx(cyc)
+    assert v["ceiling_ms"] == pytest.approx(cyc * 256 / 2.4e9 * 1e3)
     assert v["frac"] == pytest.approx(v["ceiling_ms"] / 2.0)
+    assert v["classes_per_wave"]["B32"] == pytest.approx(1560.0)
 
 
 def test_committed_pmc_matches_the_built_library(bench):

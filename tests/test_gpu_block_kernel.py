@@ -1,6 +1,5 @@
 """GPU parity of the one-QP-per-workgroup active-set kernel for the n <= 128
-class (qpb_gi_gram.hip; the round-1 kernel qpb_gi_block.hip behind
-QPB_FLAG_DIAG_BLOCK): 32 < n <= 128, m <= 256, including BASELINE configs[3]'s
+class (qpb_gi_gram.hip): 32 < n <= 128, m <= 256, including BASELINE configs[3]'s
 shape n=128, m=256.
 Oracle: oracle.active_set_solve (KKT-certified primal active set) per QP;
 x within 1e-6 relative, active set bit-exact, multipliers within 1e-6, and the
@@ -57,16 +56,6 @@ def test_block_kernel_unconstrained(qpb):
     x, lam, act, st, it = _solve(qpb, H, f)
     assert (st == qpb.OK).all()
     assert _relerr(x, np.linalg.solve(H, -f[..., None])[..., 0]).max() <= 1e-9
-
-
-def test_round1_block_kernel_still_agrees(qpb):
-    """The round-1 kernel (QPB_FLAG_DIAG_BLOCK, kept for A/B runs) on one shape."""
-    H, f, A, b = O.family_conditioned(2000 + 48 + 96, 4, 48, m=96, box=10.0, kind="box")
-    x, lam, act, st, it = _solve(qpb, H, f, A, b, flags=qpb.FLAG_DIAG_BLOCK)
-    x2, lam2, act2, st2, it2 = _solve(qpb, H, f, A, b)
-    assert (st == qpb.OK).all() and (st2 == qpb.OK).all()
-    assert np.abs(x - x2).max() <= 1e-9 * max(1.0, np.abs(x2).max())
-    assert np.array_equal(act, act2)
 
 
 @pytest.mark.parametrize("kind", ["box", "dense"])

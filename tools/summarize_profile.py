@@ -37,9 +37,40 @@ if "FETCH_SIZE_KiB_per_launch" in res and "WRITE_SIZE_KiB_per_launch" in res:
     write = res["WRITE_SIZE_KiB_per_launch"] * 1024
     res["hbm_bytes_per_launch"] = fetch + write
     res["correction"] = "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section)"
+# SQ counter groups: per-wave averages over the solver kernel's launches
+sq = {}
+for d in sorted(os.listdir(out_dir)) if os.path.isdir(out_dir) else []:
+    if not d.startswith("pmc_sq"):
+        continue
+    per = {}
+    for r in rows(os.path.join(out_dir, d, "run_counter_collection.csv")):
+        if KERNEL in r["Kernel_Name"]:
+            per.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    for k, v in per.items():
+        sq[k] = sum(v) / len(v)
+if sq.get("SQ_WAVES"):
+    res["sq_per_wave"] = {k: v / sq["SQ_WAVES"] for k, v in sq.items() if k != "SQ_WAVES"}
+    res["sq_waves_per_launch"] = sq["SQ_WAVES"]
 try:
     res["bench"] = json.loads(open(os.path.join(out_dir, "bench.json")).read().strip().splitlines()[-1])
     res["library"] = res["bench"].get("library")
 except Exception:  # noqa: BLE001
     pass
+# the candidate profiles/pmc_traffic.json (bench.py's roofline.traffic and
+# valu_ceiling), keyed to the hot kernel's revision token of the library string
+if "hbm_bytes_per_launch" in res and "sq_per_wave" in res and res.get("library"):
+    lib = res["library"]
+    inner = lib.split("(", 1)[1].rsplit(")", 1)[0]
+    rev = next(t.split(":", 1)[0].strip() for t in inner.split(";") if t.strip().startswith("gi_dense"))
+    spw = res["sq_per_wave"]
+    cfg = res["bench"]["config"]
+    pmc = {"config": {"n": cfg["n"], "m": cfg["m"], "batch_per_gpu": cfg["batch_per_gpu"], "family": cfg["family"]},
+           "library": lib, "kernel_rev": rev, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
+           "source": f"{out_dir} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, 2*FETCH+WRITE)",
+           "valu_classes": {"VALU": spw.get("SQ_INSTS_VALU"), "FMA_F64": spw.get("SQ_INSTS_VALU_FMA_F64"),
+                            "MUL_F64": spw.get("SQ_INSTS_VALU_MUL_F64"), "ADD_F64": spw.get("SQ_INSTS_VALU_ADD_F64"),
+                            "TRANS_F64": spw.get("SQ_INSTS_VALU_TRANS_F64")},
+           "valu_source": f"{out_dir} (rocprofv3 --pmc SQ_INSTS_VALU[_FMA_F64|_MUL_F64|_ADD_F64|_TRANS_F64] "
+                          f"SQ_WAVES, {rev})"}
+    json.dump(pmc, open(os.path.join(out_dir, "pmc_traffic.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
