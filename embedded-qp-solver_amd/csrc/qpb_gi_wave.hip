@@ -3,19 +3,27 @@
 // Same method as qpb_gi.hip (dual active set of Goldfarb & Idnani on
 // D = A L^{-T}, see there), mapped one QP per 64-lane wavefront: lane l owns
 // row l of D, every per-QP scalar is wave-uniform, so control flow never
-// diverges and no QP waits for another.  Broadcasts from one lane use
-// v_readlane (SGPR results) or LDS.
+// diverges and no QP waits for another.  Single values from one lane are
+// broadcast by v_readlane (SGPR results).  Selection: dual steepest edge
+// (-s / |D[l, q:]|) as in qpb_gi.hip, 14.94 -> 13.83 iterations per QP on
+// the configs[4] batch.
 //
 // Setup, one right-looking sweep as in qpb_gi.hip, except that the pivot row
 // is gathered by symmetry: row k of the Schur complement is its column k, and
 // element k of a lane's row is a compile-time register index -- every lane
-// stores it, all lanes read the vector back (one b64 store + b128 broadcast
-// reads per step, no lane-selected writes).  Row r of H / L is split over the
+// stores it (one b64 store per step, no lane-selected writes).  Row r of H / L is split over the
 // two wave halves (lane r: columns 0-15, lane r + 32: columns 16-31), so the
 // upper half carries half the Schur update instead of idling, and the row
 // costs 32 VGPRs instead of 64 (the sweep's spills went from 104 to 25 dwords;
 // 6.30 -> 5.88 ms at B = 262,144 with bitwise the same output,
 // profiles/r02/s4/ab_n32_half_sweep.json).
+//
+// Vectors every lane needs whole (the sweep's pivot column, row p of D, the
+// Householder vector, y) are held as a DPP operand pair -- entry j at lane
+// j & 15 of every 16-lane row -- and enter the FMAs by their own row_newbcast
+// (v_fmac_f64_dpp): the LDS only carries two b64 reads per lane per vector,
+// not 16 broadcast b128 reads per product (round 3: 5.86 -> 4.64 ms at
+// B = 262,144, profiles/r03/n32/ab_wave_v4.json).
 //
 // LDS per QP (one wave): L packed rows (n(n+1)/2), R column-major NP x NP with
 // zero diagonal, the pivot / exchange vector, the y / x capture.
@@ -65,31 +73,20 @@ __device__ __forceinline__ double dot2(FX &&x, FY &&y, double init = 0.0) {
   return a0 + a1;
 }
 
-__device__ __forceinline__ void lds_vec(const double *src, double (&dst)[NP]) {
-#pragma unroll
-  for (int j = 0; j < NP; j += 2) {
-    const double2 v = *reinterpret_cast<const double2 *>(&src[j]);
-    dst[j] = v.x;
-    dst[j + 1] = v.y;
-  }
+// D[l,:] . v for a vector held as v[j] = vA at lane j (j < 16) and vB at
+// lane j - 16 (j >= 16) of every 16-lane row: the FMA takes v[j] by its own
+// DPP broadcast (row_newbcast), four accumulators.  The caller has issued
+// dpp_ready on a VALU-written vA / vB.
+__device__ __forceinline__ double bdot(const double (&E)[NP], double vA, double vB) {
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  unroll<NH>([&](auto J) {
+    constexpr int j = J;
+    fmac_bc<j>(a[j & 1], vA, E[j]);
+    fmac_bc<j>(a[2 + (j & 1)], vB, E[NH + j]);
+  });
+  return (a[0] + a[1]) + (a[2] + a[3]);
 }
-
-// sum over lanes 0-31 (wave-uniform)
-__device__ __forceinline__ double half_sum(double v) {
-  v = row_sum(v);
-  return readlane_d(v, 0) + readlane_d(v, 16);
-}
-// E . (vector in LDS), two accumulators
-__device__ __forceinline__ double dot_xch(const double (&E)[NP], const double *x) {
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-  for (int j = 0; j < NP; j += 2) {
-    const double2 v = *reinterpret_cast<const double2 *>(&x[j]);
-    a0 = __builtin_fma(E[j], v.x, a0);
-    a1 = __builtin_fma(E[j + 1], v.y, a1);
-  }
-  return a0 + a1;
-}
+__device__ __forceinline__ void dpp_ready2(double a, double b) { asm volatile("s_nop 1" ::"v"(a), "v"(b)); }
 
 // one QP per wavefront; MR = 1 (m <= 64); OCC waves per SIMD
 // REDO: solve only the QPs the mixed-precision kernel marked (status
@@ -209,8 +206,8 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   clk.tick(0);  // load
   const double nrm2 = dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return E[j]; });
   const double bl = rowok ? bv : 0.0;
-  const double invn = nrm2 > 0.0 ? rsq(nrm2) : 0.0;
-  double thr = (rowok && nrm2 > 0.0) ? -feas_tol * (1.0 + __builtin_fabs(bl) * invn) : -kInf;
+  // violated: s / |D row| < -tol (1 + |b| / |D row|), i.e. s < -tol (|D row| + |b|)
+  const double thr = (rowok && nrm2 > 0.0) ? -feas_tol * (nrm2 * rsq(nrm2) + __builtin_fabs(bl)) : -kInf;
   const bool infeasible0 =
       wave_any(rowok && nrm2 == 0.0 && bl < -feas_tol * (1.0 + __builtin_fabs(bl)));
   const double fl = l < n ? fv : 0.0;
@@ -222,40 +219,16 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // Split rows: lane (h, r) = (l >> 5, l & 31) holds S[r][16h .. 16h + 15] of
   // the Schur complement.  Step k: every lane stores its entry kk = k % 16 at
   // pv[32h + r], so column k (= pivot row k by symmetry) is pv[32 kh + .],
-  // kh = k / 16, and each lane also reads its own S[r][k] there.  The half
+  // kh = k / 16.  Lane l reads two entries of it, PA = S[l & 15][k] and
+  // PB = S[16 + (l & 15)][k] (the same pair in every 16-lane row), and the
+  // updates take S[j][k] from lane j & 15 of the row by the FMA's own DPP
+  // broadcast: the pivot row is neither held nor streamed from LDS.  The half
   // owning column k scales it into L[r][k]; entries left of it are final L
   // (zero coefficient ch on the lower half), entries right of it take the
-  // Schur update.  Pivot pairs stream from LDS in double-buffered groups as
-  // below; for k < 16 the lower and upper halves read their own pairs.
+  // Schur update.
   const bool hi = l >= NP;
-  const int r = l & (NP - 1);
+  const int r = l & (NP - 1), li = l & (NH - 1);
   double *pv = R + 2 * NP;  // R is free until the loop (R[0..31]: y capture)
-  auto stream = [&](const double *src, auto NPAIRc, auto &&apply, auto &&pin_pair) {
-    constexpr int NPAIR = decltype(NPAIRc)::value, GP = 4, NG = (NPAIR + GP - 1) / GP;
-    if constexpr (NPAIR > 0) {
-      double2 buf[2][GP];
-      auto fetch = [&](auto G) {
-        constexpr int g = G;
-        unroll<GP>([&](auto I) {
-          constexpr int pr = g * GP + I;
-          if constexpr (pr < NPAIR) buf[g & 1][I] = *reinterpret_cast<const double2 *>(&src[2 * pr]);
-        });
-      };
-      fetch(std::integral_constant<int, 0>{});
-      unroll<NG>([&](auto G) {
-        constexpr int g = G;
-        if constexpr (g + 1 < NG) fetch(std::integral_constant<int, g + 1>{});
-        unroll<GP>([&](auto I) {
-          constexpr int pr = g * GP + I;
-          if constexpr (pr < NPAIR) apply(std::integral_constant<int, pr>{}, buf[g & 1][I]);
-        });
-        unroll<GP>([&](auto I) {
-          constexpr int pr = g * GP + I;
-          if constexpr (pr < NPAIR) pin_pair(std::integral_constant<int, pr>{});
-        });
-      });
-    }
-  };
   unroll<NP>([&](auto K) {
     constexpr int k = K, kh = k / NH, kk = k % NH;
     if (k >= n) return;  // wave-uniform: padded columns stay zero
@@ -263,70 +236,49 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     wave_lds_sync();
     pv[l] = Lr[kk];
     wave_lds_sync();
+    const double PA = pv[NP * kh + li], PB = pv[NP * kh + NH + li];
     const double akk = pv[NP * kh + k];
-    const double srk = pv[NP * kh + r];  // S[r][k]
+    const double srk = (r & NH) ? PB : PA;  // S[r][k]
     spd = spd && (akk > 0.0);
     const double ik = rsq(akk);
     const double ik2 = ik * ik;
     const double c = srk * ik2;
     const double ch = hi ? c : 0.0;
     const double e = E[k];
-    const double e2 = e * ik2;
+    const double me2 = -(e * ik2);
     E[k] = e * ik;
-    constexpr int j0 = (k + 1) / 2 * 2;
+    pin(E[k]);  // scaled here: sunk to the sweep's exit, the 1/sqrt pivots stay live (spills)
+    // D row: columns j > k
+    unroll<NP - 1 - k>([&](auto JJ) {
+      constexpr int j = k + 1 + JJ;
+      if constexpr (j < NH) fmac_bc<j>(E[j], PA, me2);
+      else fmac_bc<j - NH>(E[j], PB, me2);
+    });
+    const double mc = -c, mch = -ch;
     if constexpr (kh == 0) {
-      // Lr: own half's pairs (per-lane addresses), all 16 entries
-      stream(pv + NH * (l >> 5), std::integral_constant<int, NH / 2>{},
-             [&](auto PR, double2 v) {
-               constexpr int pr = PR;
-               unroll<2>([&](auto T) {
-                 constexpr int jj = 2 * pr + T;
-                 const double vj = T == 0 ? v.x : v.y;
-                 if constexpr (jj < kk) Lr[jj] = __builtin_fma(-ch, vj, Lr[jj]);
-                 else if constexpr (jj == kk) Lr[jj] = hi ? __builtin_fma(-c, vj, Lr[jj]) : Lr[jj] * ik;
-                 else Lr[jj] = __builtin_fma(-c, vj, Lr[jj]);
-               });
-             },
-             [&](auto PR) {
-               constexpr int pr = PR;
-               pin(Lr[2 * pr]);
-               pin(Lr[2 * pr + 1]);
-             });
-      // D row: columns j > k
-      stream(pv + j0, std::integral_constant<int, (NP - j0) / 2>{},
-             [&](auto PR, double2 v) {
-               constexpr int j = j0 + 2 * PR;
-               if constexpr (j >= k + 1) E[j] = __builtin_fma(-e2, v.x, E[j]);
-               E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
-             },
-             [&](auto PR) {
-               constexpr int j = j0 + 2 * PR;
-               if constexpr (j >= k + 1) pin(E[j]);
-               pin(E[j + 1]);
-             });
+      // entry jj of the lane's half is column 16h + jj: S[16h + jj][k] is
+      // lane jj's PA (lower half) or PB (upper half)
+      const double Ph = hi ? PB : PA;
+      dpp_ready(Ph);
+      unroll<NH>([&](auto JJ) {
+        constexpr int jj = JJ;
+        if constexpr (jj < kk) {
+          fmac_bc<jj>(Lr[jj], Ph, mch);
+        } else if constexpr (jj == kk) {
+          double u = Lr[jj];
+          fmac_bc<jj>(u, Ph, mc);
+          Lr[jj] = hi ? u : Lr[jj] * ik;
+        } else {
+          fmac_bc<jj>(Lr[jj], Ph, mc);
+        }
+      });
     } else {
       Lr[kk] = hi ? Lr[kk] * ik : Lr[kk];
-      // one stream feeds the D row (columns j > k) and the upper half's
-      // entries j - 16 (the lower half's are final: ch = 0 there)
-      stream(pv + NP + j0, std::integral_constant<int, (NP - j0) / 2>{},
-             [&](auto PR, double2 v) {
-               constexpr int j = j0 + 2 * PR;
-               if constexpr (j >= k + 1) {
-                 E[j] = __builtin_fma(-e2, v.x, E[j]);
-                 Lr[j - NH] = __builtin_fma(-ch, v.x, Lr[j - NH]);
-               }
-               E[j + 1] = __builtin_fma(-e2, v.y, E[j + 1]);
-               Lr[j + 1 - NH] = __builtin_fma(-ch, v.y, Lr[j + 1 - NH]);
-             },
-             [&](auto PR) {
-               constexpr int j = j0 + 2 * PR;
-               if constexpr (j >= k + 1) {
-                 pin(E[j]);
-                 pin(Lr[j - NH]);
-               }
-               pin(E[j + 1]);
-               pin(Lr[j + 1 - NH]);
-             });
+      // the upper half's entries j - 16 (the lower half's are final: ch = 0)
+      unroll<NP - 1 - k>([&](auto JJ) {
+        constexpr int j = k + 1 + JJ;
+        fmac_bc<j - NH>(Lr[j - NH], PB, mch);
+      });
     }
     const double fk = readlane_d(ya, k);
     ya = __builtin_fma(-c, fk, ya);
@@ -348,10 +300,9 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   });
   // y replicated: s = b + D y, |D row|^2
   wave_lds_sync();
-  double yv[NP];
-  lds_vec(R, yv);
-  double s = dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return yv[j]; }, bl);
+  double s = bl + bdot(E, R[li], R[NH + li]);
   const double dn = dot2<NP>([&](int j) { return E[j]; }, [&](int j) { return E[j]; });
+  float fn2 = (float)dn;  // |D[l, q:]|^2, the free part of the row (scale of the selection key)
 
   // ------------------------------------------------------ active-set loop
   wave_lds_sync();
@@ -371,11 +322,11 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   while (!done && it < max_iter) {
     ++it;
     if (selecting) {
-      const double v = s * invn;
-      const bool viol = !act && v < thr;
-      // the fp32 magnitude of the (negative) normalised slack with the row in
-      // the low 6 bits (0 = none violated), as in qpb_gi.hip
-      uint32_t kk = viol ? ((__float_as_uint((float)(-v)) & ~63u) | (uint32_t)l) : 0u;
+      // dual steepest edge as in qpb_gi.hip: the most violated row by
+      // -s / |D[l, q:]| (fp32), the row in the low 6 bits (0 = none violated)
+      const bool viol = !act && s < thr;
+      const float kf = (float)(-s) * __builtin_amdgcn_rsqf(fn2);  // fn2 >= 0 (clamped where it shrinks)
+      uint32_t kk = viol ? ((__float_as_uint(kf) & ~63u) | (uint32_t)l) : 0u;
       kk = row_max_u32(kk);
       const uint32_t k0 = __builtin_amdgcn_readlane(kk, 0), k1 = __builtin_amdgcn_readlane(kk, 16);
       const uint32_t k2 = __builtin_amdgcn_readlane(kk, 32), k3 = __builtin_amdgcn_readlane(kk, 48);
@@ -394,20 +345,20 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     if (l == p) {
 #pragma unroll
       for (int j = 0; j < NP; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[j], E[j + 1]);
-      xch[NP] = s;
-      xch[NP + 1] = dn;
+      *reinterpret_cast<double2 *>(&xch[NP]) = make_double2(s, dn);
     }
     wave_lds_sync();
-    const double Dpl = xch[l & (NP - 1)];
+    // row p as the DPP operand pair (entry j at lane j & 15 of every row),
+    // d2 = its columns >= q
+    const double XA = xch[li], XB = xch[NH + li];
     const double Dpq = xch[q < NP ? q : 0];
-    const double sp = xch[NP];
-    const double dd = xch[NP + 1];
-    wave_lds_sync();
-    if (l < q) xch[l] = 0.0;
-    // |d2|^2 from the lanes' own entries (lanes 0-31; rows 2, 3 repeat them)
-    const double nd2 = half_sum((l & (NP - 1)) >= q ? Dpl * Dpl : 0.0);
+    const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NP]);
+    const double sp = spdd.x, dd = spdd.y;
+    const double Dpl = (l & NH) ? XB : XA;  // D[p][l], lanes 0-31
+    const double d2A = li >= q ? XA : 0.0, d2B = li + NH >= q ? XB : 0.0;
+    dpp_ready2(d2A, d2B);
+    const double nd2 = row_sum(__builtin_fma(d2A, d2A, d2B * d2B));  // |d2|^2
     const double dl = (l < NP) ? -Dpl : 0.0;
-    wave_lds_sync();
 
     clk.tick(4);  // exchange
     // r = R^{-1} d1 over the active positions (position j in lane j)
@@ -438,7 +389,11 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       break;
     }
     // d2 is streamed from the exchange row (broadcast reads), not held
-    if (t2 < kBig) s = __builtin_fma(t, dot_xch(E, xch), s);
+    double ud = 0.0;  // D[l,:] . d2
+    if (t2 < kBig) {
+      ud = bdot(E, d2A, d2B);
+      s = __builtin_fma(t, ud, s);
+    }
     pin(s);
     um = __builtin_fma(-t, rm, um);
     up += t;
@@ -449,20 +404,24 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       const double nrm = nd2 * rsq(nd2);
       const double alpha = Dpq <= 0.0 ? -nrm : nrm;
       const double beta = rcp(__builtin_fma(alpha, Dpq, nd2));
-      wave_lds_sync();
-      if (l == q) xch[q] = Dpq + alpha;
-      wave_lds_sync();
-      const double w = beta * dot_xch(E, xch);
-#pragma unroll
-      for (int j = 0; j < NP; j += 2) {
-        const double2 v = *reinterpret_cast<const double2 *>(&xch[j]);
-        E[j] = __builtin_fma(-w, v.x, E[j]);
-        E[j + 1] = __builtin_fma(-w, v.y, E[j + 1]);
-      }
+      const double ia = rcp(alpha);
+      // the reflection maps e_q to -d2 / alpha: the new column q is -ud / alpha
+      // and leaves the free part, whose norm the reflection otherwise keeps
+      const float cq = (float)(ud * ia);
+      fn2 = __builtin_fmaxf(__builtin_fmaf(-cq, cq, fn2), 0.0f);
+      // v = d2 + alpha e_q in the DPP operand pair; E -= beta (E . v) v^T
+      const double vA = d2A + (li == q ? alpha : 0.0), vB = d2B + (li + NH == q ? alpha : 0.0);
+      dpp_ready2(vA, vB);
+      const double mw = -beta * bdot(E, vA, vB);
+      unroll<NH>([&](auto J) {
+        constexpr int j = J;
+        fmac_bc<j>(E[j], vA, mw);
+        fmac_bc<j>(E[NH + j], vB, mw);
+      });
       if (l < NP) R[q * NP + l] = (l < q) ? dl : 0.0;
       if (l == q) {
         rdg = alpha;
-        invRd = rcp(alpha);
+        invRd = ia;
         iam = p;
         um = up;
       }
@@ -486,14 +445,24 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       const int lc = l & (NP - 1);
       wave_lds_sync();
       if (l < q) R[l * NP + l] = rdg;
-      const bool shift = l >= k && l < q - 1;
-      for (int i = 0; i < q; ++i) {
+      // columns k+1 .. q-1 move left by one, column q-1 clears: lane l copies
+      // column l+1 whole (rows >= q are zero), half a column per pass (DS
+      // instructions run in order, so each read precedes every lane's write)
+      const bool shift = l >= k && l < q - 1, clear = l == q - 1;
+      unroll<2>([&](auto Hh) {
+        constexpr int i0 = NH * Hh;
+        double2 col[NH / 2];
         wave_lds_sync();
-        const double nxt = R[((lc + 1) & (NP - 1)) * NP + i];
+        unroll<NH / 2>([&](auto I) {
+          col[I] = *reinterpret_cast<const double2 *>(&R[((lc + 1) & (NP - 1)) * NP + i0 + 2 * I]);
+        });
         wave_lds_sync();
-        if (shift) R[l * NP + i] = nxt;
-        else if (l == q - 1) R[l * NP + i] = 0.0;
-      }
+        if (shift || clear) {
+          unroll<NH / 2>([&](auto I) {
+            *reinterpret_cast<double2 *>(&R[lc * NP + i0 + 2 * I]) = clear ? make_double2(0.0, 0.0) : col[I];
+          });
+        }
+      });
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
         const double a = R[j * NP + j], bb = R[j * NP + j + 1];
@@ -518,6 +487,14 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
           }
         });
       }
+      // column q-1 rejoins the free part
+      unroll<NP>([&](auto JJ) {
+        constexpr int jj = JJ;
+        if (jj == q - 1) {
+          fn2 = __builtin_fmaf((float)E[jj], (float)E[jj], fn2);
+          asm volatile("; fn %0" ::"n"(jj));
+        }
+      });
       wave_lds_sync();
       if (l < NP) R[l * NP + q - 1] = 0.0;
       --q;

@@ -62,7 +62,9 @@ def main(names):
         st = sols[nm].status
         out[nm] = {"median_us": round(t[len(t) // 2], 1), "min_us": round(t[0], 1),
                    "redo_frac": float((st == qpb.STATUS_REDO).double().mean()),
-                   "ok_frac": float((st == qpb.OK).double().mean())}
+                   "ok_frac": float((st == qpb.OK).double().mean()),
+                   "iters_mean": float(sols[nm].iters.double().mean()),
+                   "x_maxdiff_vs_first": float((sols[nm].x - sols[names[0]].x).abs().max())}
     print(json.dumps({"B": B, "family": fam, "variants": out}, indent=1))
 
 

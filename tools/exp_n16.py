@@ -3,7 +3,8 @@
 kernel time (HIP events, median), with the inputs read from L2 only
 (QPB_FLAG_DIAG_L2), with max_iter = 1 / 2 / 4, the iteration histogram and
 the 4-QP lockstep trip count, and the per-section wave ticks of the stamped
-build.  usage: exp_n16.py [B] [family]"""
+build.  usage: exp_n16.py [B] [family]; N=32 runs the n=32, m=64 wave kernel
+(configs[4] shape, one QP per wave, default generator scales)"""
 import json
 import os
 import sys
@@ -15,10 +16,14 @@ import torch  # noqa: E402
 
 import qpb  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
-fam = sys.argv[2] if len(sys.argv) > 2 else "box"
+N = int(os.environ.get("N", 16))
+B = int(sys.argv[1]) if len(sys.argv) > 1 else (1 << 20 if N <= 16 else 262144)
+fam = sys.argv[2] if len(sys.argv) > 2 else ("box" if N <= 16 else "dense")
 dev = torch.device("cuda", 0)
-H, f, A, b = qpb.generate(16, B, 20261015, family=fam, shift=1.0, box=10.0)
+if N <= 16:
+    H, f, A, b = qpb.generate(N, B, 20261015, family=fam, shift=1.0, box=10.0)
+else:
+    H, f, A, b = qpb.generate(N, B, 20261015, family=fam)
 sol = qpb.solve(H, f, A, b)
 torch.cuda.synchronize()
 
@@ -60,8 +65,9 @@ qpb.solve_sections(H, f, A, b, sec, out=sol)
 e.record()
 torch.cuda.synchronize()
 v = sec.cpu().tolist()
-waves = B // 4
-out["sections_us_per_wave"] = {nm: round(x / waves / 100.0, 3) for nm, x in zip(qpb.SECTION_NAMES, v)}
+waves = B // 4 if N <= 16 else B
+names = qpb.SECTION_NAMES if N <= 16 else qpb.WAVE_SECTION_NAMES
+out["sections_us_per_wave"] = {nm: round(x / waves / 100.0, 3) for nm, x in zip(names, v)}
 out["stamped_kernel_ms"] = a.elapsed_time(e)
 out["mean_resident_waves"] = round(sum(v) / 100.0 / (a.elapsed_time(e) * 1e3), 1)
 print(json.dumps(out, indent=1))

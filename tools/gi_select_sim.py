@@ -1,7 +1,8 @@
 # Goldfarb-Idnani dual active-set in numpy (the kernel's formulation) with
 # selectable constraint-selection rules; counts iterations (ADD + DROP).
-import sys, numpy as np
-sys.path.insert(0, '/root/repo/oracle')
+# usage: N=32 python tools/gi_select_sim.py [B] [family] [rules...]
+import os, sys, numpy as np
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'oracle'))
 import oracle
 
 def gi(H, f, A, b, rule, tol=1e-10):
@@ -62,7 +63,7 @@ def gi(H, f, A, b, rule, tol=1e-10):
 
 if __name__ == '__main__':
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
-    H, f, A, b = oracle.family_generate(16, B, 20261015, family=sys.argv[2] if len(sys.argv) > 2 else 'box', shift=1.0, box=10.0)
+    H, f, A, b = oracle.family_generate(int(os.environ.get('N', 16)), B, 20261015, family=sys.argv[2] if len(sys.argv) > 2 else 'box', shift=1.0, box=10.0)
     base = None
     for rule in sys.argv[3:] or ['anorm', 'dnorm', 'raw', 'proj']:
         its = []; dr = []; Ws = []
