@@ -23,7 +23,11 @@
 // j & 15 of every 16-lane row -- and enter the FMAs by their own row_newbcast
 // (v_fmac_f64_dpp): the LDS only carries two b64 reads per lane per vector,
 // not 16 broadcast b128 reads per product (round 3: 5.86 -> 4.64 ms at
-// B = 262,144, profiles/r03/n32/ab_wave_v4.json).
+// B = 262,144, profiles/r03/n32/ab_wave_v4.json).  The loop's back
+// substitution runs in the same layout (4.63 -> 4.57 ms), and R's column
+// stride is padded to 34 doubles: DROP's row-wise reads and writes were 16-
+// to 32-way bank conflicts, 1 400 of them per QP (PMC), now 35 (4.54 ->
+// 4.44 ms, profiles/r03/n32/ab_wave_rstride.json).
 //
 // LDS per QP (one wave): L packed rows (n(n+1)/2), R column-major NP x NP with
 // zero diagonal, the pivot / exchange vector, the y / x capture.
@@ -41,9 +45,12 @@ constexpr int NP = 32;                              // padded n
 constexpr int NH = NP / 2;                          // H / L row half held per lane
 constexpr int L_SIZE = NP * (NP + 1) / 2;           // 528
 constexpr int OFF_L = 0;
-constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*NP + i
-constexpr int OFF_X = OFF_R + NP * NP;              // 1552: exchange row (NP) + s_p, |d|^2; pivots
-constexpr int SLOT = OFF_X + NP + 8;                // 1592 doubles = 12,736 B
+constexpr int RS = NP + 2;                          // R column stride: row-wise reads and writes
+                                                    // (DROP's Givens, the column shift) stay
+                                                    // conflict-free, columns 16-byte aligned
+constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*RS + i
+constexpr int OFF_X = OFF_R + NP * RS;              // 1616: exchange row (NP) + s_p, |d|^2; pivots
+constexpr int SLOT = OFF_X + NP + 8;                // 1656 doubles = 13,248 B (12 waves per CU)
 constexpr double kDepTol = 1e-24;
 
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
@@ -306,9 +313,10 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
 
   // ------------------------------------------------------ active-set loop
   wave_lds_sync();
-  for (int j = 0; j < NP; ++j) R[j * NP + (l & (NP - 1))] = 0.0;
+  for (int j = 0; j < NP; ++j) R[j * RS + (l & (NP - 1))] = 0.0;
   int q = 0;
-  double um = 0.0, rdg = 0.0, invRd = 0.0;
+  double um = 0.0, rdg = 0.0;
+  double ninvA = 0.0, ninvB = 0.0;  // -1 / R_jj of positions j = l & 15 and 16 + (l & 15)
   int iam = -1;
   bool act = false;
   int status = !spd ? QPB_NOT_SPD : (infeasible0 ? QPB_INFEASIBLE : QPB_MAX_ITER);
@@ -361,15 +369,39 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     const double dl = (l < NP) ? -Dpl : 0.0;
 
     clk.tick(4);  // exchange
-    // r = R^{-1} d1 over the active positions (position j in lane j)
+    // r = R^{-1} d1 over the active positions, in the DPP layout: lane i of
+    // every row carries positions i (nA) and 16 + i (nB), on the negated
+    // accumulator n = -acc (n_l += R[l][j] r_j, r_j = n_j * (-1 / R_jj)); r_j
+    // enters the FMAs by their own DPP broadcast from lane j & 15.  Steps run
+    // in groups of four columns whose R entries are read up front; a step
+    // j >= q adds zeros (n_j = 0, column j of R is zero).
     double rm = 0.0;
     if (q > 0) {
-      double acc = (l < q) ? dl : 0.0;
-      for (int j = q - 1; j >= 0; --j) {
-        const double rj = readlane_d(acc * invRd, j);
-        acc = __builtin_fma(-R[j * NP + (l & (NP - 1))], rj, acc);
-      }
-      rm = acc * invRd;
+      double nA = li < q ? XA : 0.0, nB = li + NH < q ? XB : 0.0;  // -d1 = D[p][0:q]
+      unroll<NP / 4>([&](auto G) {
+        constexpr int j0 = NP - 4 - 4 * G;
+        if (j0 < q) {
+          double ra[4], rb[4];
+          unroll<4>([&](auto I) {
+            constexpr int j = j0 + 3 - I;
+            ra[I] = R[j * RS + li];
+            if constexpr (j >= NH) rb[I] = R[j * RS + NH + li];
+          });
+          unroll<4>([&](auto I) {
+            constexpr int j = j0 + 3 - I;
+            if constexpr (j >= NH) {
+              const double tj = nB * ninvB;
+              fmac_bc_nop<j - NH>(nA, tj, ra[I]);
+              fmac_bc<j - NH>(nB, tj, rb[I]);
+            } else {
+              const double tj = nA * ninvA;
+              fmac_bc_nop<j>(nA, tj, ra[I]);
+            }
+          });
+        }
+      });
+      const double rA = nA * ninvA, rB = nB * ninvB;
+      rm = (l < q) ? ((l & NH) ? rB : rA) : 0.0;
     }
     clk.tick(5);  // back solve
     double t1 = kBig;
@@ -418,13 +450,14 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
         fmac_bc<j>(E[j], vA, mw);
         fmac_bc<j>(E[NH + j], vB, mw);
       });
-      if (l < NP) R[q * NP + l] = (l < q) ? dl : 0.0;
+      if (l < NP) R[q * RS + l] = (l < q) ? dl : 0.0;
       if (l == q) {
         rdg = alpha;
-        invRd = ia;
         iam = p;
         um = up;
       }
+      if (li == q) ninvA = -ia;
+      if (li + NH == q) ninvB = -ia;
       if (l == p) act = true;
       ++q;
       selecting = true;
@@ -444,7 +477,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       }
       const int lc = l & (NP - 1);
       wave_lds_sync();
-      if (l < q) R[l * NP + l] = rdg;
+      if (l < q) R[l * RS + l] = rdg;
       // columns k+1 .. q-1 move left by one, column q-1 clears: lane l copies
       // column l+1 whole (rows >= q are zero), half a column per pass (DS
       // instructions run in order, so each read precedes every lane's write)
@@ -454,25 +487,25 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
         double2 col[NH / 2];
         wave_lds_sync();
         unroll<NH / 2>([&](auto I) {
-          col[I] = *reinterpret_cast<const double2 *>(&R[((lc + 1) & (NP - 1)) * NP + i0 + 2 * I]);
+          col[I] = *reinterpret_cast<const double2 *>(&R[((lc + 1) & (NP - 1)) * RS + i0 + 2 * I]);
         });
         wave_lds_sync();
         if (shift || clear) {
           unroll<NH / 2>([&](auto I) {
-            *reinterpret_cast<double2 *>(&R[lc * NP + i0 + 2 * I]) = clear ? make_double2(0.0, 0.0) : col[I];
+            *reinterpret_cast<double2 *>(&R[lc * RS + i0 + 2 * I]) = clear ? make_double2(0.0, 0.0) : col[I];
           });
         }
       });
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
-        const double a = R[j * NP + j], bb = R[j * NP + j + 1];
+        const double a = R[j * RS + j], bb = R[j * RS + j + 1];
         const double ir = rsq(__builtin_fma(a, a, bb * bb));
         const double cj = a * ir, sj = bb * ir;
-        const double rj = R[lc * NP + j], rj1 = R[lc * NP + j + 1];
+        const double rj = R[lc * RS + j], rj1 = R[lc * RS + j + 1];
         wave_lds_sync();
         if (l >= j && l < q - 1) {
-          R[l * NP + j] = __builtin_fma(cj, rj, sj * rj1);
-          R[l * NP + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
+          R[l * RS + j] = __builtin_fma(cj, rj, sj * rj1);
+          R[l * RS + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
         }
         // the same rotation on columns j, j+1 of D (j wave-uniform)
         unroll<NP - 1>([&](auto JJ) {
@@ -496,14 +529,16 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
         }
       });
       wave_lds_sync();
-      if (l < NP) R[l * NP + q - 1] = 0.0;
+      if (l < NP) R[l * RS + q - 1] = 0.0;
       --q;
       wave_lds_sync();
-      const double dg = (l < q) ? R[l * NP + l] : 0.0;
+      const double dg = (l < q) ? R[l * RS + l] : 0.0;
+      const double dgA = R[li * RS + li], dgB = R[(NH + li) * RS + NH + li];
       wave_lds_sync();
-      if (l < q) R[l * NP + l] = 0.0;
+      if (l < q) R[l * RS + l] = 0.0;
       rdg = dg;
-      invRd = (l < q) ? rcp(dg) : 0.0;
+      ninvA = li < q ? -rcp(dgA) : 0.0;
+      ninvB = li + NH < q ? -rcp(dgB) : 0.0;
       clk.tick(8);  // drop
     }
   }
