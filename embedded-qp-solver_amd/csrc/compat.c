@@ -50,24 +50,56 @@ static int g_init;
 static struct slot g_nxn[POOL_NXN], g_nx1[POOL_NX1], g_qf[POOL_QF];
 static double *g_nxn_store, *g_nx1_store;
 
+/* The sanitizer build (Makefile target asan) gives every pool matrix its own
+ * heap block, so an access past one matrix's elements is a heap overflow
+ * AddressSanitizer reports, not a silent read of the neighbouring matrix. */
+#if defined(__SANITIZE_ADDRESS__)
+#define QPB_POOL_PER_SLOT 1
+#elif defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#define QPB_POOL_PER_SLOT 1
+#endif
+#endif
+#ifndef QPB_POOL_PER_SLOT
+#define QPB_POOL_PER_SLOT 0
+#endif
+
+static void pool_release(void)
+{
+#if QPB_POOL_PER_SLOT
+	if (g_init) {
+		for (int i = 0; i < POOL_NXN; i++)
+			free(g_nxn[i].v.m.elements);
+		for (int i = 0; i < POOL_NX1; i++)
+			free(g_nx1[i].v.m.elements);
+	}
+#endif
+	free(g_nxn_store);
+	free(g_nx1_store);
+	g_nxn_store = g_nx1_store = NULL;
+}
+
 void qpb_compat_init(unsigned n_dim, double admm_box_min, double admm_box_max)
 {
 	if (n_dim == 0 || n_dim > 65535)
 		n_dim = 48;
-	free(g_nxn_store);
-	free(g_nx1_store);
+	pool_release();
 	g_ndim = n_dim;
 	g_box_min = admm_box_min;
 	g_box_max = admm_box_max;
+#if !QPB_POOL_PER_SLOT
 	g_nxn_store = calloc((size_t)POOL_NXN * n_dim * n_dim, sizeof(double));
 	g_nx1_store = calloc((size_t)POOL_NX1 * n_dim, sizeof(double));
+#endif
 	for (int i = 0; i < POOL_NXN; i++) {
 		g_nxn[i].used = 0;
-		g_nxn[i].v.m.elements = g_nxn_store + (size_t)i * n_dim * n_dim;
+		g_nxn[i].v.m.elements = QPB_POOL_PER_SLOT ? calloc((size_t)n_dim * n_dim, sizeof(double))
+							  : g_nxn_store + (size_t)i * n_dim * n_dim;
 	}
 	for (int i = 0; i < POOL_NX1; i++) {
 		g_nx1[i].used = 0;
-		g_nx1[i].v.m.elements = g_nx1_store + (size_t)i * n_dim;
+		g_nx1[i].v.m.elements = QPB_POOL_PER_SLOT ? calloc(n_dim, sizeof(double))
+							  : g_nx1_store + (size_t)i * n_dim;
 	}
 	for (int i = 0; i < POOL_QF; i++)
 		g_qf[i].used = 0;

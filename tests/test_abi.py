@@ -10,7 +10,9 @@ import pytest
 
 from conftest import ROOT
 
-LIB = os.path.join(ROOT, "embedded-qp-solver_amd", "lib", "libqpb.so")
+# QPB_LIB: another build of the same library (tests/test_sanitizers.py runs
+# this file against the ASan/UBSan build)
+LIB = os.environ.get("QPB_LIB", os.path.join(ROOT, "embedded-qp-solver_amd", "lib", "libqpb.so"))
 HEADERS = [os.path.join(ROOT, "include", "qpb.h")] + [
     os.path.join(ROOT, "include", "compat", h) for h in ("kmalloc.h", "matrix_ops.h", "qp.h", "qp_solvers.h")]
 
@@ -75,8 +77,7 @@ def test_argument_errors_without_gpu():
     d = Desc(16, 32, 0, 0, 0, 0.0)
     assert lib.qpb_solve(ctypes.byref(d), *([None] * 10)) == 0
     # a real call with no device fails loudly (never a CPU fallback)
-    import torch
-    if not torch.cuda.is_available():
+    if not _device_present():
         d = Desc(16, 32, 4, 0, 0, 0.0)
         buf = ctypes.create_string_buffer(64)
         p = ctypes.cast(buf, vp)
@@ -96,8 +97,7 @@ def test_box_argument_errors_without_gpu():
     assert b"qpb_solve" in lib.qpb_last_error()
     d = Desc(16, 32, 0, 0, 0, 0.0)
     assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == 0
-    import torch
-    if not torch.cuda.is_available():
+    if not _device_present():
         d = Desc(16, 32, 4, 0, 0, 0.0)
         buf = ctypes.create_string_buffer(64)
         p = ctypes.cast(buf, vp)
@@ -105,6 +105,16 @@ def test_box_argument_errors_without_gpu():
         assert lib.qpb_solve_box(ctypes.byref(d), p, p, None, None, p, p, p, p, None, None) == -4
 
 
+def _device_present():
+    # under the sanitizer run torch stays out of the process (it is not
+    # instrumented and only answers this question); that run is CPU-only
+    if os.environ.get("QPB_SANITIZED"):
+        return False
+    import torch
+    return torch.cuda.is_available()
+
+
+@pytest.mark.skipif(bool(os.environ.get("QPB_SANITIZED")), reason="imports torch")
 def test_python_binding_imports():
     import qpb
     assert qpb.version().startswith("qpb")

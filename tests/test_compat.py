@@ -10,7 +10,9 @@ import pytest
 
 from conftest import GOLDEN, ROOT
 
-LIB = os.path.join(ROOT, "embedded-qp-solver_amd", "lib", "libqpb.so")
+# QPB_LIB: another build of the same library (tests/test_sanitizers.py runs
+# this file against the ASan/UBSan build)
+LIB = os.environ.get("QPB_LIB", os.path.join(ROOT, "embedded-qp-solver_amd", "lib", "libqpb.so"))
 NxN, Nx1, QF = 0, 1, 2
 
 

@@ -14,7 +14,7 @@ sol = qpb.solve(H, f); torch.cuda.synchronize()
 t0 = time.perf_counter()
 for _ in range(3): sol = qpb.solve(H, f)
 torch.cuda.synchronize(); print("m=0", (time.perf_counter() - t0) / 3 * 1e3, "ms")
-names = ["chol", "D", "y+s", "select+v", "r+ratio", "w", "step+update", "outputs", "L restore", "x", "queue", "H load", "diag", "panel", "trailing", "step:t", "step:gemv", "step:upd", "step:keys"]
+names = ["chol", "D", "y+s", "select", "d", "w+r", "step+update", "outputs", "L restore", "x", "queue", "H load", "diag", "panel", "trailing", "step:t", "step:gemv", "step:upd", "step:keys"]
 sec = torch.zeros(20, dtype=torch.int64, device="cuda")
 sol = qpb.solve(H, f, A, b)
 qpb.solve_sections(H, f, A, b, sec, out=sol); torch.cuda.synchronize()
