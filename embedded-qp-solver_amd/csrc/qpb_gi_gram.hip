@@ -1,8 +1,8 @@
 // qpb_gi_gram.hip -- active-set QP kernel for 32 < n <= 128, m <= 256 (gfx950).
 //
 // BASELINE configs[3] (n = 128, m = 256).  The same dual active-set method as
-// qpb_gi.hip (Goldfarb & Idnani), restated on the Gram matrix of the
-// constraint rows so that the big operand never changes after the setup:
+// qpb_gi.hip (Goldfarb & Idnani) with D = A L^{-T} fixed after the setup and
+// the active set's factorisation kept beside it:
 //
 //   setup   H = L L^T (blocked, right-looking, 16 x 16 tiles: trailing updates
 //           and panel solves on the fp64 matrix cores, v_mfma_f64_16x16x4_f64),
@@ -10,18 +10,18 @@
 //           the diagonal-tile solves on the matrix cores), y = L^{-1} f,
 //           s = b + D y (the slack of the unconstrained minimiser,
 //           test/qp_ref.py:35's answer).
-//   iterate for the selected row p (most violated normalised slack):
-//           u = D[p,:], v = D u (= column p of G = D D^T), c = v[W],
-//           r = G_WW^{-1} c (explicit inverse, updated by bordering),
-//           w = u - D_W^T r, |w|^2 (= |d2|^2 of G-I), slack direction D w,
-//           partial step t1 (ratio test on the multipliers), full step
-//           t2 = -s_p / |w|^2, s += t D w.
-//           ADD p: G_WW^{-1} grows by the bordering formula, D_W gains row u.
-//           DROP k: G_WW^{-1} loses row / column k by the Schur-complement
-//           downdate, D_W loses row k.  D itself is never rotated: the
-//           factor updates are O(q^2), the per-iteration big work is two
-//           GEMVs with D (v = D u and D w).
-//   finish  x = -L^{-T} (y + D_W^T lam) (KKT stationarity), L recomputed.
+//   iterate for the selected row p (most violated normalised slack), with
+//           D_W^T = Q1^T R (Q1: orthonormal rows, R upper triangular, kept as
+//           Z = R^{-1}):
+//           u = D[p,:], d = Q1 u, w = u - Q1^T d (|w|^2 = |d2|^2 of G-I),
+//           r = Z d, slack direction D w, partial step t1 (ratio test on the
+//           multipliers), full step t2 = -s_p / |w|^2, s += t D w.
+//           ADD p: Q1 gains the row w / |w|, Z the column [-r / |w|; 1 / |w|].
+//           DROP k: Givens rotations zero row k of Z (columns k .. q-1), the
+//           same rotations on Q1's rows, row k of Z goes.  Every phase is a
+//           parallel pass; no triangular solve and nothing O(q^2) per ADD.
+//   finish  x = -L^{-T} (y + D^T lam) (KKT stationarity, lam by row), L
+//           restored from the scratch.
 //
 // Replaces, batched, the reference's dense kernels on this path: matrix_mult
 // (matrix_ops.c:235-271) as the MFMA tile products and the GEMVs, the LU /
@@ -37,15 +37,12 @@
 // D[32w + 16t + j][16k + g + 4r] (element r), i.e. in each row tile row j,
 // the 32 columns congruent to g mod 4.  A row dot product is 32 FMAs and two
 // cross-group butterfly steps.
-// LDS (160 KiB): the packed lower triangle (L in setup and finish, G_WW^{-1}
-// in the loop), the diagonal-tile inverses (setup) / the active rows D_W
+// LDS (160 KiB): the packed triangle (L in setup and finish, Z = R^{-1} by
+// columns in the loop), the diagonal-tile inverses (setup) / the rows of Q1
 // (loop; rows past QL live in a per-workgroup global scratch), vectors.
 #include "qpb_common.h"
 #include "qpb.h"
 
-#ifndef GRAM_PUB_ROWS
-#define GRAM_PUB_ROWS 0  // 1: every wave publishes its candidate row (session-4 form)
-#endif
 #ifndef GRAM_BC
 #define GRAM_BC 1
 #endif
@@ -65,25 +62,28 @@ constexpr int NBUF = 2136;
 constexpr int OFF_TRI = 0;
 constexpr int OFF_ROWS = LP;  // diagonal-tile inverses (setup) / D_W rows (loop)
 constexpr int OFF_BUF = LDS_D - NBUF;
-constexpr int QL = (OFF_BUF - OFF_ROWS) / NB;  // D_W rows in LDS (79)
+// Q1 rows in LDS at stride QS: 2 QS = 32 mod 64 dwords, so the row-adjacent
+// lane groups of one b64 read (the d and w phases) hit opposite bank halves
+constexpr int QS = 144;
+constexpr int QL = (OFF_BUF - OFF_ROWS) / QS;  // Q1 rows in LDS (70)
 // Permuted vectors (u, w, y) keep lane group g's 32 entries at 34 g: the four
 // groups' b128 reads then start 4 banks apart instead of on the same banks.
 constexpr int B_CAND = OFF_BUF;                // per wave: its most violated row of D (PV each)
 constexpr int B_CSP = B_CAND + NWV * PV;       // per wave: that row's slack
 constexpr int B_W = B_CSP + NWV;               // w (padded permuted)
-constexpr int B_V = B_W + PV;                  // v = D u (by row); lambda scatter at the end
-constexpr int B_R = B_V + MB;                  // r by slot
-constexpr int B_CB = B_R + NB;                 // c = v[W] by slot
-constexpr int B_LAM = B_CB + NB;               // multipliers by slot
+constexpr int B_V = B_W + PV;                  // DROP scratch (row k of Z); lambda scatter at the end
+constexpr int B_R = B_V + MB;                  // r by position
+constexpr int B_CB = B_R + NB;                 // d = Q1 u by position
+constexpr int B_LAM = B_CB + NB;               // multipliers by position
 constexpr int B_Y = B_LAM + NB;                // y (padded permuted), then y + D_W^T lam
 constexpr int B_RED = B_Y + PV;                // selection keys, partial reductions, scalars
 constexpr int B_INT = B_RED + 32;              // ints: flags, queue slot, mask words (64)
-constexpr int B_IAM = B_INT + 32;              // ints: constraint index by slot (128)
+constexpr int B_IAM = B_INT + 32;              // ints: constraint index by position (128)
 static_assert(B_IAM + 64 == LDS_D, "LDS layout");
 static_assert(OFF_ROWS + 8 * 256 <= OFF_BUF, "diagonal-tile inverses fit the row area");
 // B_RED slots
 constexpr int R_KEY = 0;    // per-wave selection keys (NWV)
-constexpr int R_T1 = 8;     // per-wave (ratio min, argmin slot) pairs (2 NWV)
+constexpr int R_T1 = 8;     // per-wave (ratio min, argmin position) pairs (2 NWV)
 constexpr int R_ND2 = 24;   // per-wave partial |w|^2 (NWV)
 constexpr double kDepTol = 1e-24;
 constexpr long long SCRATCH = LP + (long long)(NB - QL) * NB;  // doubles per workgroup
@@ -430,11 +430,11 @@ __device__ __forceinline__ void solve_upper(const double *Lp, int nb, int l, dou
   a1 *= id1;
 }
 
-// ------------------------------------------------------ D_W row storage
+// ------------------------------------------------------- Q1 row storage
 struct Rows {
-  double *lds;  // rows 0..QL-1
-  double *gl;   // rows QL.. (per-workgroup global scratch)
-  __device__ __forceinline__ double *row(int j) const { return j < QL ? lds + j * NB : gl + (j - QL) * NB; }
+  double *lds;  // rows 0..QL-1, stride QS
+  double *gl;   // rows QL.. (per-workgroup global scratch), stride NB
+  __device__ __forceinline__ double *row(int j) const { return j < QL ? lds + j * QS : gl + (j - QL) * NB; }
 };
 
 // ------------------------------------------------------------------ kernel
@@ -449,15 +449,15 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
   // s, 3 select + v, 4 r + ratio, 5 w, 6 step + update, 7 outputs, 8 L again,
   // 9 x, 10 queue)
   SectionClock<STAMP> clk;
-  double *Lp = lds + OFF_TRI;  // L, then G_WW^{-1} (packed lower)
+  double *Lp = lds + OFF_TRI;  // L, then Z = R^{-1} (packed by columns)
   double *LI = lds + OFF_ROWS;
   double *wb = lds + B_W, *vb = lds + B_V, *rb = lds + B_R, *lamb = lds + B_LAM, *yb = lds + B_Y;
   double *red = lds + B_RED;
   int *flags = reinterpret_cast<int *>(lds + B_INT);
   int *iamb = reinterpret_cast<int *>(lds + B_IAM);
-  // per-workgroup scratch: L (packed), then the D_W rows past QL
+  // per-workgroup scratch: L (packed), then the Q1 rows past QL
   double *Lgl = scratch + (long long)blockIdx.x * SCRATCH;
-  const Rows DW{lds + OFF_ROWS, Lgl + LP};
+  const Rows QR{lds + OFF_ROWS, Lgl + LP};
   const int T = (n + 15) >> 4, nb = 16 * T;
   bool first = true;
   for (;;) {
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     continue;
 #endif
     // L kept in the workgroup's scratch for the final solve (the triangle
-    // holds G_WW^{-1} during the loop); the loads back come after several
+    // holds Z = R^{-1} during the loop); the loads back come after several
     // barriers on the same CU
 #pragma unroll
     for (int u = 0; u < (LP + NT - 1) / NT; ++u) {
@@ -586,7 +586,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     clk.tick(1);
     double invn[RT], thr[RT], s[RT];
     bool zero_bad = false, act[RT];
-    int slot[RT];  // the active-set slot of this lane's row, -1 if inactive
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       const double nn2 = group_sum(na2[t]);
@@ -594,7 +593,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       thr[t] = (rowok[t] && nn2 > 0.0) ? -feas_tol * (1.0 + __builtin_fabs(bl[t]) * invn[t]) : -kInf;
       zero_bad = zero_bad || (rowok[t] && nn2 == 0.0 && bl[t] < -feas_tol * (1.0 + __builtin_fabs(bl[t])));
       act[t] = false;
-      slot[t] = -1;
     }
     if (tid == 0) flags[20] = 0;
     __syncthreads();
@@ -627,20 +625,29 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     }
 
     // ------------------------------------------------------- active set
-    // The active constraints live in SLOTS (0 .. hi-1, occupancy mask occ):
-    // slot j holds a row index (iamb), its multiplier (lamb), its row of D
-    // (D_W) and row / column j of G_WW^{-1} (zero for free slots, so sums
-    // may run over every slot below hi).  A DROP frees a slot, an ADD takes
-    // the lowest free one: nothing is ever shifted.  Row i of the packed
-    // inverse belongs to threads 8 (i mod NT/8) + c, columns c, c + 8, ...
-    int it = 0, p = 0, hi = 0;
-    unsigned long long occ0 = 0, occ1 = 0;  // slot occupancy (uniform)
+    // G-I's J = L^{-T} [Q1^T Q2] in the form D_W^T = Q1^T R, with R kept as
+    // its inverse Z = R^{-1}: the orthonormal rows Q1 (q x n, permuted column
+    // order; LDS rows at stride QS, rows past QL in the scratch) and the upper
+    // triangular Z (q x q, packed by columns in the triangle: Z[i][j] at
+    // tri(j, i)), positions 0 .. q-1 in the order of the active set.  For the
+    // selected row u = D[p,:] one iteration is
+    //   d = Q1 u                        (G-I's d1 = J1^T n+)
+    //   w = u - Q1^T d, |w|^2, r = Z d  (J2 J2^T n+, |d2|^2, R^{-1} d1; one
+    //                                    phase: w and r do not wait for each other)
+    //   D w, the step; ADD: Q1 gains the row w / |w|, Z the column
+    //   [-r / |w|; 1 / |w|] (the bordered inverse); DROP k: Givens rotations
+    //   on Z's columns j, j+1 (j = k .. q-2) chosen to zero row k of Z, the
+    //   same rotations on Q1's rows, then row k of Z and the last column and
+    //   row go (R with column k removed, re-triangularised, inverted).
+    // Every phase is a parallel pass: nothing is O(q^2) per ADD, and no
+    // triangular solve runs in the loop.
+    int it = 0, p = 0, q = 0;
     bool selecting = true;
-    double up = 0.0;
+    double up = 0.0, dd = 0.0;
     const double *ub = lds + B_CAND;  // u = D[p,:]: the winning wave's candidate row
+    double *db = lds + B_CB;          // d by position
     // each wave offers its most violated row: the key (normalised slack, row
-    // in the low mantissa bits), the row of D (padded permuted) and its slack,
-    // so the next selection needs no broadcast round of its own
+    // in the low mantissa bits) and its slack
     auto publish_key = [&]() {
       double key = kBig;
 #pragma unroll
@@ -651,32 +658,16 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       key = row_min(key);  // the 16 rows of each tile pair, on every lane group
       if (l == 0) red[R_KEY + wv] = key;
       const int pw = key_index256(key);
-#if GRAM_PUB_ROWS
-      if (key < kBig) {
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-          if (row[t] == pw) {  // the four lanes of the candidate row
-            double *dst = lds + B_CAND + wv * PV + 34 * lk;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              *reinterpret_cast<double2 *>(&dst[4 * k]) = make_double2(E[t][k][0], E[t][k][1]);
-              *reinterpret_cast<double2 *>(&dst[4 * k + 2]) = make_double2(E[t][k][2], E[t][k][3]);
-            }
-            if (lk == 0) lds[B_CSP + wv] = s[t];
-          }
-      }
-#else
       // the row itself is written after the selection, by its wave only
       if (key < kBig) {
 #pragma unroll
         for (int t = 0; t < RT; ++t)
           if (row[t] == pw && lk == 0) lds[B_CSP + wv] = s[t];
       }
-#endif
     };
     if (tid < NB) {
       iamb[tid] = -1;
-      lds[B_CB + tid] = 0.0;
+      db[tid] = 0.0;
     }
     if (!done) publish_key();
     __syncthreads();
@@ -693,13 +684,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         p = key_index256(kmin);
         up = 0.0;
         selecting = false;
-#if GRAM_PUB_ROWS
-        ub = lds + B_CAND + (p / (16 * RT)) * PV;
-#else
-        // u = D[p,:] from the one wave that holds row p (an extra barrier is
-        // cheap; eight waves each storing a candidate row through four lanes
-        // kept the LDS store path busy)
-        ub = lds + B_CAND;
+        // u = D[p,:] from the one wave that holds row p
         if (wv == p / (16 * RT)) {
 #pragma unroll
           for (int t = 0; t < RT; ++t)
@@ -713,74 +698,67 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
             }
         }
         __syncthreads();
-#endif
-        double vr[RT];
-        row_dot(E, ub + 34 * lk, vr);  // v = D u: column p of G
-        if (lk == 0) {
-#pragma unroll
-          for (int t = 0; t < RT; ++t) {
-            vb[row[t]] = vr[t];
-            if (slot[t] >= 0) lds[B_CB + slot[t]] = vr[t];  // c = v[W], by slot
-          }
-        }
-        __syncthreads();
+        // |u|^2 (the dependency test's scale) on every wave
+        const double ua = ub[pad(l)], ubb = ub[pad(l + 64)];
+        dd = wave_sum(__builtin_fma(ua, ua, ubb * ubb));
       }
       clk.tick(3);
-      // ---- r = G_WW^{-1} v[W] and the ratio test on every wavefront: lane
-      // (g, j) of wave w takes slot t = 16 w + j over the columns i = g mod 4
-      // (group sums finish the dot products)
+      // ---- d = Q1 u: lane (lk, li) of wave w takes position 32 j + 4 w + lk
+      // over the columns li + 16 i (row sums over the 16 lanes finish it)
+      for (int t0 = 4 * wv; t0 < q; t0 += 4 * NWV) {
+        const int t = t0 + lk;
+        const double *qr = QR.row(t < q ? t : t0);
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+          a0 = __builtin_fma(qr[li + 16 * i], ub[pad(li + 16 * i)], a0);
+          a1 = __builtin_fma(qr[li + 16 * i + 16], ub[pad(li + 16 * i + 16)], a1);
+        }
+        const double dv = row_sum(a0 + a1);
+        if (li == 0 && t < q) db[t] = dv;
+      }
+      __syncthreads();
+      clk.tick(4);
+      // ---- w = u - Q1^T d: lane (lk, li) of wave w takes (permuted) column
+      // 16 w + li over the positions j = lk mod 4; |w|^2 per wave
       {
-        const int t = 16 * wv + li;
+        const int c = 16 * wv + li;
         double acc0 = 0.0, acc1 = 0.0;
-        const double *cb = lds + B_CB;  // free slots: zero rows of G_WW^{-1}
-        for (int i = lk; i < hi; i += 8) {
-          const bool two = i + 4 < hi;
-          const double g0 = sym(Lp, t, i), g2 = two ? sym(Lp, t, i + 4) : 0.0;
-          acc0 = __builtin_fma(g0, cb[i], acc0);
-          acc1 = __builtin_fma(g2, two ? cb[i + 4] : 0.0, acc1);
+        const int qa = q < QL ? q : QL;
+        int j = lk;
+        for (; j + 4 < qa; j += 8) {
+          acc0 = __builtin_fma(db[j], QR.lds[j * QS + c], acc0);
+          acc1 = __builtin_fma(db[j + 4], QR.lds[(j + 4) * QS + c], acc1);
         }
-        const double rt = group_sum(acc0 + acc1);
+        if (j < qa) acc0 = __builtin_fma(db[j], QR.lds[j * QS + c], acc0);
+        for (j = QL + lk; j < q; j += 4) acc1 = __builtin_fma(db[j], QR.gl[(j - QL) * NB + c], acc1);
+        const double w = ub[pad(c)] - group_sum(acc0 + acc1);
+        if (lk == 0) wb[pad(c)] = w;
+        const double ws = wave_sum(lk == 0 ? w * w : 0.0);
+        if (l == 0) red[R_ND2 + wv] = ws;
+      }
+      // ---- r = Z d over rows i = 16 w + li (lane group lk: the columns
+      // c >= i, c = lk mod 4), then each wave's ratio minimum (first position
+      // at the minimum; waves in position order)
+      {
+        const int i = 16 * wv + li;
         double ratio = kBig;
-        if (t < hi) {
-          if (lk == 0) rb[t] = rt;
-          const bool occupied = ((t < 64 ? occ0 >> t : occ1 >> (t - 64)) & 1ull) != 0;
-          if (rt > 0.0 && occupied) ratio = lamb[t] * rcp(rt);
+        if (16 * wv < q) {
+          double acc = 0.0;
+          int c = lk + ((i > lk) ? ((i - lk + 3) & ~3) : 0);
+          for (; c < q; c += 4) acc = __builtin_fma(Lp[tri(c, i)], db[c], acc);
+          const double rt = group_sum(acc);
+          if (i < q) {
+            if (lk == 0) rb[i] = rt;
+            if (rt > 0.0) ratio = lamb[i] * rcp(rt);
+          }
         }
-        const double wmin = row_min(ratio);  // the wave's 16 slots (every row holds them)
-        // first slot reaching the minimum
-        const double kpos = row_min((ratio == wmin && wmin < kBig) ? (double)t : 1e9);
+        const double wmin = row_min(ratio);
+        const double kpos = row_min((ratio == wmin && wmin < kBig) ? (double)i : 1e9);
         if (l == 0) {
           red[R_T1 + 2 * wv] = wmin;
           red[R_T1 + 2 * wv + 1] = kpos;
         }
-      }
-      __syncthreads();
-      clk.tick(4);
-      // ---- w = u - D_W^T r: lane (g, j) of wave w takes (permuted) column
-      // 16 w + j over the slots j' = g mod 4; |w|^2 per wave
-      {
-        const int c = 16 * wv + li;
-        double acc0 = 0.0, acc1 = 0.0;
-        const int ha = hi < QL ? hi : QL;
-        int j = lk;
-        for (; j + 4 < ha; j += 8) {
-          acc0 = __builtin_fma(-rb[j], DW.lds[j * NB + c], acc0);
-          acc1 = __builtin_fma(-rb[j + 4], DW.lds[(j + 4) * NB + c], acc1);
-        }
-        if (j < ha) acc0 = __builtin_fma(-rb[j], DW.lds[j * NB + c], acc0);
-        for (j = QL + lk; j < hi; j += 4) acc1 = __builtin_fma(-rb[j], DW.gl[(j - QL) * NB + c], acc1);
-        const double uc = ub[pad(c)];
-        const double w = uc + group_sum(acc0 + acc1);
-        if (lk == 0) {
-          wb[pad(c)] = w;
-          // u into the D_W row of the slot an ADD would take (harmless if this
-          // step turns out a DROP: a free slot's r is 0); the candidate rows
-          // are rewritten in the step phase
-          const int anext = ~occ0 ? __builtin_ctzll(~occ0) : 64 + __builtin_ctzll(~occ1);
-          DW.row(anext)[c] = uc;
-        }
-        const double ws = wave_sum(lk == 0 ? w * w : 0.0);
-        if (l == 0) red[R_ND2 + wv] = ws;
       }
       __syncthreads();
       clk.tick(5);
@@ -791,12 +769,11 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       double nd2 = 0.0;
 #pragma unroll
       for (int w = 0; w < NWV; ++w) nd2 += red[R_ND2 + w];
-      const double dd = vb[p];
       const double sp = lds[B_CSP + p / (16 * RT)];
       double t1 = kBig;
       int kdrop = 0;
 #pragma unroll
-      for (int w = 0; w < NWV; ++w)  // waves in slot order: ties keep the lowest slot
+      for (int w = 0; w < NWV; ++w)  // waves in position order: ties keep the lowest position
         if (red[R_T1 + 2 * w] < t1) {
           t1 = red[R_T1 + 2 * w];
           kdrop = (int)red[R_T1 + 2 * w + 1];
@@ -814,60 +791,102 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       }
       up += tt;
       clk.tick(16);
-      if (tid < hi) lamb[tid] = __builtin_fma(-tt, rb[tid], lamb[tid]);  // free slots: r = 0
+      if (tid < q) lamb[tid] = __builtin_fma(-tt, rb[tid], lamb[tid]);
       if (t2 <= t1) {
-        // ---- ADD p in the lowest free slot a: G_WW^{-1} bordered
-        const int a = ~occ0 ? __builtin_ctzll(~occ0) : 64 + __builtin_ctzll(~occ1);
-        const int hn = a + 1 > hi ? a + 1 : hi;
-        const double inv = 1.0 / nd2;
-        for (int i = tid >> 3; i < hi; i += NT / 8) {  // + r r^T / |w|^2 off slot a
-          const double ri = rb[i] * inv;
-          double *gi = Lp + tri(i, 0);
-          if (i != a)
-            for (int j = tid & 7; j <= i; j += 8)
-              if (j != a) gi[j] = __builtin_fma(ri, rb[j], gi[j]);
-        }
-        if (tid < hn) Lp[tid >= a ? tri(tid, a) : tri(a, tid)] = tid == a ? inv : -rb[tid] * inv;
+        // ---- ADD p at position q
+        const double rn = rsq(nd2);  // 1 / |w|
+        if (tid < NB) QR.row(q)[tid] = wb[pad(tid)] * rn;
+        if (tid < q) Lp[tri(q, tid)] = -rb[tid] * rn;
+        if (tid == q) Lp[tri(q, q)] = rn;
         if (tid == 0) {
-          iamb[a] = p;
-          lamb[a] = up;
+          iamb[q] = p;
+          lamb[q] = up;
         }
-        if (a < 64) occ0 |= 1ull << a;
-        else occ1 |= 1ull << (a - 64);
-        hi = hn;
 #pragma unroll
         for (int t = 0; t < RT; ++t)
-          if (row[t] == p) {
-            act[t] = true;
-            slot[t] = a;
-          }
+          if (row[t] == p) act[t] = true;
+        ++q;
         selecting = true;
       } else {
-        // ---- DROP slot k: Schur-complement downdate of G_WW^{-1} on the
-        // other slots, then row / column k cleared
+        // ---- DROP position k
         const int k = kdrop;
         const int cdrop = iamb[k];
 #pragma unroll
         for (int t = 0; t < RT; ++t)
-          if (row[t] == cdrop) {
-            act[t] = false;
-            slot[t] = -1;
+          if (row[t] == cdrop) act[t] = false;
+        // row k of Z (columns k .. q-1) copied aside: the rotation chains of
+        // waves 0-2 read it while wave 0 rewrites Z in place
+        double *zrow = vb + NB;
+        if (tid >= k && tid < q) zrow[tid] = Lp[tri(tid, k)];
+        __syncthreads();  // the multiplier update above and zrow, before the shift
+        // Rotation j (j = k .. q-2) on the pair (j, j+1) zeroes Z[k][j]: with
+        // X_k = Z[k][k] and X_{j+1} = hypot(X_j, Z[k][j+1]) (the carried
+        // entry of row k), c_j = Z[k][j+1] / X_{j+1}, s_j = -X_j / X_{j+1}.
+        // Every wave that applies rotations runs this scalar chain itself.
+        if (wv == 0) {
+          // Z's columns: lane l carries rows l and l + 64; row i > k moves to
+          // i - 1 (row k goes).  Step j reads column j+1 and writes column j;
+          // one wave's DS instructions run in order, so the row moving into
+          // i - 1 never overwrites an entry row i - 1 has still to read.
+          double x0 = l <= k ? Lp[tri(k, l <= k ? l : 0)] : 0.0;  // rows' entries in column k
+          double x1 = l + 64 <= k ? Lp[tri(k, l + 64 <= k ? l + 64 : 0)] : 0.0;
+          double X = zrow[k];
+          for (int j = k; j < q - 1; ++j) {
+            const double z0 = l <= j + 1 ? Lp[tri(j + 1, l <= j + 1 ? l : 0)] : 0.0;
+            const double z1 = l + 64 <= j + 1 ? Lp[tri(j + 1, l + 64 <= j + 1 ? l + 64 : 0)] : 0.0;
+            const double zk = zrow[j + 1];
+            const double h = __builtin_sqrt(__builtin_fma(X, X, zk * zk));
+            const double ih = 1.0 / h;
+            const double cs = zk * ih, sn = -X * ih;
+            const double n0 = __builtin_fma(cs, x0, sn * z0), n1 = __builtin_fma(cs, x1, sn * z1);
+            x0 = __builtin_fma(-sn, x0, cs * z0);
+            x1 = __builtin_fma(-sn, x1, cs * z1);
+            X = h;
+            wave_lds_sync();
+            // new row i' = i (i < k) or i - 1 (i > k), column j: rows <= j only
+            const int i0 = l < k ? l : l - 1, i1 = l + 64 < k ? l + 64 : l + 63;
+            if (l != k && i0 <= j && l <= j + 1) Lp[tri(j, i0)] = n0;
+            if (l + 64 != k && i1 <= j && l + 64 <= j + 1) Lp[tri(j, i1)] = n1;
           }
-        const double ikk = 1.0 / Lp[tri(k, k)];
-        for (int i = tid >> 3; i < hi; i += NT / 8) {
-          if (i == k) continue;
-          const double gik = sym(Lp, i, k) * ikk;
-          for (int j = tid & 7; j <= i; j += 8)
-            if (j != k) Lp[tri(i, j)] = __builtin_fma(-gik, sym(Lp, j, k), Lp[tri(i, j)]);
+        } else if (wv == 1 || wv == 2) {
+          // Q1's rows, one column per thread
+          const int c = tid - 64;
+          if (k < q - 1) {
+            double X = zrow[k];
+            double cur = QR.row(k)[c];
+            for (int j = k; j < q - 1; ++j) {
+              const double zk = zrow[j + 1];
+              const double nx = QR.row(j + 1)[c];
+              const double h = __builtin_sqrt(__builtin_fma(X, X, zk * zk));
+              const double ih = 1.0 / h;
+              const double cs = zk * ih, sn = -X * ih;
+              QR.row(j)[c] = __builtin_fma(cs, cur, sn * nx);
+              cur = __builtin_fma(-sn, cur, cs * nx);
+              X = h;
+            }
+          }
+        } else if (wv == 3) {
+          // positions k+1 .. q-1 move down by one (reads before writes: one
+          // wave's DS instructions run in order)
+          const double l0 = lamb[l + 1], l1 = lamb[l + 64 < NB - 1 ? l + 65 : NB - 1];
+          const int i0 = iamb[l + 1], i1 = iamb[l + 64 < NB - 1 ? l + 65 : NB - 1];
+          wave_lds_sync();
+          if (l >= k && l < q - 1) {
+            lamb[l] = l0;
+            iamb[l] = i0;
+          } else if (l == q - 1) {
+            lamb[l] = 0.0;
+            iamb[l] = -1;
+          }
+          if (l + 64 >= k && l + 64 < q - 1) {
+            lamb[l + 64] = l1;
+            iamb[l + 64] = i1;
+          } else if (l + 64 == q - 1) {
+            lamb[l + 64] = 0.0;
+            iamb[l + 64] = -1;
+          }
         }
-        __syncthreads();
-        if (tid < hi) Lp[tid >= k ? tri(tid, k) : tri(k, tid)] = 0.0;
-        if (tid == 0) {
-          iamb[k] = -1;
-          lamb[k] = 0.0;
-        }
-        if (k < 64) occ0 &= ~(1ull << k);
-        else occ1 &= ~(1ull << (k - 64));
+        --q;
 #pragma unroll
         for (int t = 0; t < RT; ++t)  // p stays selected: its slack after the partial step
           if (row[t] == p && lk == 0) lds[B_CSP + wv] = s[t];
@@ -882,15 +901,35 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 #pragma unroll
     for (int u = 0; u < PF; ++u) asm volatile("" ::"v"(pf[u]));
     // ------------------------------------------------------------ outputs
-    // full multiplier vector by row (vb), the active-set words, g = y + D_W^T lam
+    // full multiplier vector by row (vb), the active-set words,
+    // g = y + D_W^T lam = y + D^T lam_full: each wave sums its 32 rows of D
+    // weighted by their multipliers (16-lane row sums), the eight partial
+    // vectors are added per column
     for (int e = tid; e < MB; e += NT) vb[e] = 0.0;
     __syncthreads();
-    if (tid < hi && iamb[tid] >= 0) vb[iamb[tid]] = lamb[tid];
+    if (tid < q && iamb[tid] >= 0) vb[iamb[tid]] = lamb[tid];
+    __syncthreads();
+    {
+      double lw[RT];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) lw[t] = vb[row[t]];
+      double *part = lds + OFF_ROWS + wv * PV;  // the Q1 rows are dead now
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double a = lw[0] * E[0][k][r];
+#pragma unroll
+          for (int t = 1; t < RT; ++t) a = __builtin_fma(lw[t], E[t][k][r], a);
+          a = row_sum(a);
+          if (li == 0) part[34 * lk + 4 * k + r] = a;  // permuted column order, padded
+        }
+    }
+    __syncthreads();
     if (tid < NB) {
       double gsum = yb[pad(tid)];
-      const int ha = hi < QL ? hi : QL;
-      for (int j = 0; j < ha; ++j) gsum = __builtin_fma(lamb[j], DW.lds[j * NB + tid], gsum);
-      for (int j = QL; j < hi; ++j) gsum = __builtin_fma(lamb[j], DW.gl[(j - QL) * NB + tid], gsum);
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) gsum += lds[OFF_ROWS + w * PV + pad(tid)];
       yb[pad(tid)] = gsum;
     }
     {
@@ -903,7 +942,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     for (int e = tid; e < m; e += NT) lamg[g * m + e] = vb[e];
     const int words = (m + 31) >> 5;
     if (tid < words) actg[g * words + tid] = (uint32_t)flags[2 + tid];
-    // x = -L^{-T} g: L again (the triangle held G_WW^{-1})
+    // x = -L^{-T} g: L again (the triangle held Z)
     bool finite = true;
     clk.tick(7);
     if (spd) {
