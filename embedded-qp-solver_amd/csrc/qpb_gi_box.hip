@@ -161,10 +161,16 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
   });
   // slacks of the unconstrained minimiser x0 = -L^{-T} y: b + D y per row
   double su = bu + ey, sl = bl - ey;
+  // |D[l, q:]|^2, the free part of both of the lane's rows (scale of the
+  // selection key, as qpb_gi.hip)
+  float fn2 = (float)dot2<NL>([&](int j) { return E[j]; }, [&](int j) { return E[j]; });
 
   // ------------------------------------------------------ active-set loop
+  // zeroed in pairs at lane-rotated positions (the same position in every
+  // lane's column would be an 8-way bank conflict per store)
 #pragma unroll
-  for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&R[l * NL + j]) = make_double2(0.0, 0.0);
+  for (int j = 0; j < NL; j += 2)
+    *reinterpret_cast<double2 *>(&R[l * NL + ((j + 2 * l) & (NL - 1))]) = make_double2(0.0, 0.0);
   int q = 0;
   double um = 0.0;  // multiplier of active position l
   int iam = -1;     // constraint (0..15 upper, 16..31 lower) at active position l
@@ -180,10 +186,12 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
   while (!done && it < max_iter) {
     ++it;
     if (selecting) {
-      // most violated bound (rows have unit norm): fp32-magnitude keys with
-      // the row in the low 5 bits, DPP-fused max (qpb_gi.hip)
-      const uint32_t ku = (__float_as_uint((float)(-su)) & ~31u) | (uint32_t)l;
-      const uint32_t kl = (__float_as_uint((float)(-sl)) & ~31u) | (uint32_t)(l + NL);
+      // violated bounds (rows of unit norm) ranked by dual steepest edge,
+      // -s / |D[l, q:]| as in qpb_gi.hip (the same choices as the dense path
+      // on A = [I; -I]): fp32 keys with the row in the low 5 bits, DPP-fused max
+      const float rf = __builtin_amdgcn_rsqf(fn2);  // fn2 >= 0 (clamped where it shrinks)
+      const uint32_t ku = (__float_as_uint((float)(-su) * rf) & ~31u) | (uint32_t)l;
+      const uint32_t kl = (__float_as_uint((float)(-sl) * rf) & ~31u) | (uint32_t)(l + NL);
       uint32_t key = (!actu && su < thu) ? ku : 0u;
       key = (!actl && sl < thl && kl > key) ? kl : key;
       key = row_max_u32(key);
@@ -208,11 +216,10 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
     const double wl = xch[l];
     const double wq = xch[q];  // q == 16 reads s_p: only used by an ADD, impossible then
     const double sp = xch[NL];
-    wave_lds_sync();
-    if (l < q) xch[l] = 0.0;
-    wave_lds_sync();
-    double w2[NL];  // the selected row with its active columns zeroed; d2 = sgn * w2
-    lds_row16(xch, w2);
+    // the selected row with its active columns zeroed, entry j at lane j
+    // (d2 = sgn * w2): the products below take it by DPP broadcast
+    const double w2 = l >= q ? wl : 0.0;
+    dpp_ready(w2);
     const double Dpl = sgn * wl, Dpq = sgn * wq;
     const double dl = -Dpl;
     const double nd2 = row_sum(l >= q ? wl * wl : 0.0);  // |d2|^2
@@ -246,8 +253,14 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
       done = true;
       break;
     }
+    double u = 0.0;  // D[l,:] . d2
     if (t2 < kBig) {  // slacks s -= t D[:, q:] d2: the upper row's product, negated for the lower
-      const double u = sgn * dot2<NL>([&](int j) { return E[j]; }, [&](int j) { return w2[j]; });
+      double a0 = 0.0, a1 = 0.0;
+      unroll<NL>([&](auto J) {
+        constexpr int j = J;
+        fmac_bc<j>(j % 2 ? a1 : a0, w2, E[j]);
+      });
+      u = sgn * (a0 + a1);
       su = __builtin_fma(t, u, su);
       sl = __builtin_fma(-t, u, sl);
     }
@@ -263,17 +276,27 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
       const double nrm = nd2 * ir;
       const double alpha = Dpq <= 0.0 ? -nrm : nrm;
       const double beta = ir * rcp1(nrm + __builtin_fabs(Dpq));
-      if (l == q) xch[q] = wq + sgn * alpha;
-      wave_lds_sync();
-      double v[NL];
-      lds_row16(xch, v);
-      const double w = beta * dot2<NL>([&](int j) { return E[j]; }, [&](int j) { return v[j]; });
-#pragma unroll
-      for (int j = 0; j < NL; ++j) E[j] = __builtin_fma(-w, v[j], E[j]);
+      const double ia = Dpq <= 0.0 ? -ir : ir;  // 1 / alpha
+      // the reflection maps e_q to -d2 / alpha: column q of the new D is
+      // -u / alpha, and it leaves the free part of the row
+      const float cq = (float)(u * ia);
+      fn2 = __builtin_fmaxf(__builtin_fmaf(-cq, cq, fn2), 0.0f);
+      const double v = w2 + (l == q ? sgn * alpha : 0.0);
+      dpp_ready(v);
+      double a0 = 0.0, a1 = 0.0;
+      unroll<NL>([&](auto J) {
+        constexpr int j = J;
+        fmac_bc<j>(j % 2 ? a1 : a0, v, E[j]);
+      });
+      const double nw = -beta * (a0 + a1);
+      unroll<NL>([&](auto J) {
+        constexpr int j = J;
+        fmac_bc<j>(E[j], v, nw);
+      });
       R[q * NL + l] = (l < q) ? dl : 0.0;
       if (l == q) {
         rdg = alpha;
-        invRd = Dpq <= 0.0 ? -ir : ir;  // 1 / alpha
+        invRd = ia;
         iam = p;
         um = up;
       }
@@ -302,13 +325,22 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
       // full R (diagonal put back), delete column k (lane l owns column l)
       wave_lds_sync();
       if (l < q) R[l * NL + l] = rdg;
-      const bool shift = l >= k && l < q - 1;
-      for (int i = 0; i < qmax; ++i) {
+      // lane l copies column l+1 whole (one pass: in-order DS, every read
+      // precedes every write), pairs at lane-rotated positions (conflict-free)
+      {
+        double2 col[NL / 2];
+#pragma unroll
+        for (int t = 0; t < NL / 2; ++t)
+          col[t] = *reinterpret_cast<const double2 *>(&R[((l + 1) & (NL - 1)) * NL + ((2 * t + 2 * l) & (NL - 1))]);
         wave_lds_sync();
-        const double nxt = R[((l + 1) & (NL - 1)) * NL + i];
-        wave_lds_sync();
-        if (shift) R[l * NL + i] = nxt;
-        else if (l == q - 1) R[l * NL + i] = 0.0;
+        if (l >= k && l < q - 1) {
+#pragma unroll
+          for (int t = 0; t < NL / 2; ++t) *reinterpret_cast<double2 *>(&R[l * NL + ((2 * t + 2 * l) & (NL - 1))]) = col[t];
+        } else if (l == q - 1) {
+#pragma unroll
+          for (int t = 0; t < NL / 2; ++t)
+            *reinterpret_cast<double2 *>(&R[l * NL + ((2 * t + 2 * l) & (NL - 1))]) = make_double2(0.0, 0.0);
+        }
       }
       // Givens rotations restore the upper-triangular R ...
       for (int j = k; j < q - 1; ++j) {
@@ -338,6 +370,17 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
         }
       });
       --q;
+      // column q (after the rotations) joins the free part: recompute
+      {
+        float a0 = 0.0f, a1 = 0.0f;
+        unroll<NL>([&](auto J) {
+          constexpr int j = J;
+          const float e = (float)E[j];
+          if constexpr (j % 2 == 0) a0 = __builtin_fmaf(e, j >= q ? e : 0.0f, a0);
+          if constexpr (j % 2 == 1) a1 = __builtin_fmaf(e, j >= q ? e : 0.0f, a1);
+        });
+        fn2 = a0 + a1;
+      }
       wave_lds_sync();
       const double dg = (l < q) ? R[l * NL + l] : 0.0;
       wave_lds_sync();

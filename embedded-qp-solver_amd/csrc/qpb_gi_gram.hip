@@ -254,6 +254,12 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
     bool ok = true;
     unroll<16>([&](auto Kc) {
       constexpr int k = Kc;
+      // a step boundary the scheduler keeps (as qpb_gi.hip's sweep): the
+      // previous step's writes of a[j] (and, at k = 0, the selects above)
+      // stay ahead of this step's broadcast and rsq chain, well over the two
+      // wait states the v_fmac_f64_dpp reads of a[j] need (hipcc does not pad
+      // inline asm; tests/test_dpp_hazards.py checks the built objects)
+      __builtin_amdgcn_sched_barrier(0);
       // pivot row k of the Schur complement = column k (symmetry): lane k's
       // entries, broadcast by DPP
       const double akk = bc<k>(a[k]);
