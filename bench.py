@@ -163,14 +163,15 @@ def _cpu_worker(args):
             return done, el
 
 
-def cpu_run(fn: str, iters: int, H, f, seconds: float, procs: int):
+def cpu_run(fn: str, iters: int, H, f, seconds: float, procs: int, lib_name: str = "libqpref_n16_10.so"):
     """The compiled reference solver `fn` (oracle/ref_driver.c over the
-    unmodified qp_solvers.c) on the given QPs, one forked process per CPU
-    (the reference is not thread-safe: static pools kmalloc.c:37-42)."""
+    unmodified qp_solvers.c, built for N_DIM and the ADMM box of `lib_name`)
+    on the given QPs, one forked process per CPU (the reference is not
+    thread-safe: static pools kmalloc.c:37-42)."""
     import multiprocessing as mp
 
     import numpy as np
-    lib = os.path.join(ROOT, "oracle", "_ref", "libqpref_n16_10.so")
+    lib = os.path.join(ROOT, "oracle", "_ref", lib_name)
     if not os.path.exists(lib):
         return None
     P, q = np.ascontiguousarray(H), np.ascontiguousarray(f)

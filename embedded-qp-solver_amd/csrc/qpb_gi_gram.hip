@@ -766,6 +766,9 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           red[R_T1 + 2 * wv + 1] = kpos;
         }
       }
+      // s_p, read before the barrier: an ADD's publish_key below rewrites the
+      // candidate slacks while slower waves may still be in this step
+      const double sp = lds[B_CSP + p / (16 * RT)];
       __syncthreads();
       clk.tick(5);
       // ---- slack direction D w (issued before the scalar chain below needs it)
@@ -775,7 +778,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       double nd2 = 0.0;
 #pragma unroll
       for (int w = 0; w < NWV; ++w) nd2 += red[R_ND2 + w];
-      const double sp = lds[B_CSP + p / (16 * RT)];
       double t1 = kBig;
       int kdrop = 0;
 #pragma unroll

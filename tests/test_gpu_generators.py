@@ -83,4 +83,4 @@ def test_generator_argument_errors(qpb):
     with pytest.raises(qpb.QPBError):
         qpb.generate(16, 4, 1, m=20)  # box family needs m = 2n
     with pytest.raises(qpb.QPBError):
-        qpb.ref_generate(65, 1, 1)
+        qpb.ref_generate(129, 1, 1)  # n <= 128 (QPB_MAX_N)

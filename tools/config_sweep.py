@@ -57,7 +57,33 @@ def main():
                      "frac_of_8TBs": B * bpq / (ms * 1e-3) / 8e12, "iters_mean": float(it.mean()),
                      "iters_max": int(it.max()), "flags": flags}
         print(name, json.dumps(out[name]), file=sys.stderr, flush=True)
+    if not args or "c3_ref_newton" in args:
+        out["c3_ref_newton"] = ref_newton_n128()
+        print("c3_ref_newton", json.dumps(out["c3_ref_newton"]), file=sys.stderr, flush=True)
     print(json.dumps(out, indent=1))
+
+
+def ref_newton_n128(B=16384, cpu_qps=512, seconds=10.0):
+    """Like-for-like at configs[3]'s n = 128: the reference's own Newton
+    (qp_solvers.c:103-144, 10 iterations, x0 = 0 on both sides) on the
+    reference generator's P and q (qpb_ref_generate, srand 1), as the bitwise
+    GPU replica (qpb_ref_solve,
+    B QPs) and as the compiled reference (oracle/_ref/libqpref_n128_1e12.so,
+    one process per CPU of this job's share, on the first cpu_qps of them)."""
+    n = 128
+    P, q, _ = qpb.ref_generate(n, B, seed=1)
+    x0 = torch.zeros_like(q)
+    sol = qpb.ref_solve(qpb.REF_NEWTON, P, q, x0, iterations=10)
+    torch.cuda.synchronize()
+    ms = t_kernel(lambda: qpb.ref_solve(qpb.REF_NEWTON, P, q, x0, iterations=10), 3)
+    row = {"n": n, "batch": B, "iterations": 10, "gpu_kernel_ms": ms, "gpu_qps_per_s": B / (ms * 1e-3)}
+    procs = bench.cpu_share()
+    Pc, qc = P[:cpu_qps].cpu().numpy(), q[:cpu_qps].cpu().numpy()
+    cpu = bench.cpu_run("ref_newton_batch", 10, Pc, qc, seconds, procs, lib_name="libqpref_n128_1e12.so")
+    row.update({"cpu_reference_qps_per_s": cpu, "cpu_cores": procs, "cpu_sample_qps": cpu_qps,
+                "ratio": (B / (ms * 1e-3)) / cpu if cpu else None,
+                "bitwise_vs_reference": "tests/test_gpu_reference_modes.py (n = 128, 64 QPs)"})
+    return row
 
 
 if __name__ == "__main__":
