@@ -163,7 +163,7 @@ int qpb_ref_solve_host(const qpb_ref_desc *desc, const double *P,
 		       int32_t *iters);
 
 /* Batched matrix_invert (matrix_ops.c:551-630): Pinv = P^{-1} per matrix,
- * n <= 64, device pointers, n*n doubles each.  The reference's partial-pivot
+ * n <= 128, device pointers, n*n doubles each.  The reference's partial-pivot
  * LU (first strict maximum, physical row swaps, :434-536) and per-column
  * forward / back solves, unfused, in its order: bitwise equal to the
  * reference's result.  A singular pivot stops the LU as in the reference
@@ -195,7 +195,7 @@ int qpb_solve_sections(const qpb_desc *desc, const double *H, const double *f,
  * matrix_random (main.c:37-39 order), glibc TYPE_3 rand().  QPs
  * [first, first + batch) of that sequence (each QP jumps ahead to its own
  * offset), so any shard equals the same QPs of one sequential run.
- * P n*n, q n, x0 n per QP, device pointers.  1 <= n <= 64.              */
+ * P n*n, q n, x0 n per QP, device pointers.  1 <= n <= 128.             */
 typedef struct qpb_ref_gen_desc {
 	int32_t n;      /* N_DIM */
 	uint32_t seed;  /* srand() argument */
