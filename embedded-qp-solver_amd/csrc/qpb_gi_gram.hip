@@ -80,7 +80,12 @@ constexpr int B_RED = B_Y + PV;                // selection keys, partial reduct
 constexpr int B_INT = B_RED + 32;              // ints: flags, queue slot, mask words (64)
 constexpr int B_IAM = B_INT + 32;              // ints: constraint index by position (128)
 static_assert(B_IAM + 64 == LDS_D, "LDS layout");
-static_assert(OFF_ROWS + 8 * 256 <= OFF_BUF, "diagonal-tile inverses fit the row area");
+// diagonal-tile inverses (setup): 16 x 16 at row stride LIS = 17, so the
+// lanes of a b64 read, one row each, start 34 dwords apart (conflict-free);
+// at stride 16 every read was an 8-way bank conflict
+constexpr int LIS = 17;
+constexpr int LIT = 16 * LIS;  // doubles per tile
+static_assert(OFF_ROWS + 8 * LIT <= OFF_BUF, "diagonal-tile inverses fit the row area");
 // B_RED slots
 constexpr int R_KEY = 0;    // per-wave selection keys (NWV)
 constexpr int R_T1 = 8;     // per-wave (ratio min, argmin position) pairs (2 NWV)
@@ -286,7 +291,7 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         if (j <= i) Lp[tri(r0 + i, r0 + j)] = a[j];
-        LI[K * 256 + j * 16 + i] = e[j];
+        LI[K * LIT + j * LIS + i] = e[j];
       }
     }
     if (l == 0 && !ok) flags[0] = 1;
@@ -326,7 +331,7 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
       d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        mfma(Lp[tri(16 * I + li, 16 * K + 4 * s + lk)], LI[K * 256 + li * 16 + 4 * s + lk], acc);
+        mfma(Lp[tri(16 * I + li, 16 * K + 4 * s + lk)], LI[K * LIT + li * LIS + 4 * s + lk], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) Lp[tri(16 * I + lk + 4 * r, 16 * K + li)] = acc[r];
     }
@@ -579,7 +584,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         for (int t = 0; t < RT; ++t) Z[t] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const double a = LI[k * 256 + li * 16 + 4 * s + lk];
+          const double a = LI[k * LIT + li * LIS + 4 * s + lk];
 #pragma unroll
           for (int t = 0; t < RT; ++t) mfma(a, C[t][s], Z[t]);
         }
