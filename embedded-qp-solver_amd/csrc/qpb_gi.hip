@@ -70,12 +70,6 @@ constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: exchange rows (MR x 16), s_p, 
                                           // cos / sin (16 + 16); y / x capture; lambda scatter
 constexpr int SLOT = OFF_XCH + 34;        // 426 (4 x 426 x 8 B = 13,632 B per wave: 12 waves per CU)
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
-#ifndef QPB_XCH_ALL
-#define QPB_XCH_ALL 0  // 1: the owner writes all its rows, no VALU selects (+2.3 % box, +3.0 % dense: profiles/r03/ab/ab_v12*.json)
-#endif
-#ifndef QPB_RV_PREFETCH
-#define QPB_RV_PREFETCH 0  // R entries of the back substitution read ahead (multiple of 4, <= 16): 8 spills (+21 %)
-#endif
 static_assert(SLOT % 2 == 0 && OFF_T % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
 static_assert(4 * SLOT * 8 <= 160 * 1024 / 12, "12 waves (3 per SIMD) per CU by LDS");
 static_assert(NL * RS <= SLOT - OFF_T, "input transposes are staged in T + xch");
@@ -386,29 +380,6 @@ __device__ __forceinline__ void gi_group(
     // keeps its entry D[p][l] (d = -D[p,:] in G-I's sign convention; the
     // signs are folded into the formulas below)
     const int owner = p & (NL - 1), prow = p >> 4;
-#if QPB_XCH_ALL
-    // the owner lane writes all its MR rows (MR x 8 stores, no selects of the
-    // row on the VALU); readers index row prow
-    if (l == owner) {
-#pragma unroll
-      for (int r = 0; r < MR; ++r)
-#pragma unroll
-        for (int j = 0; j < NL; j += 2)
-          *reinterpret_cast<double2 *>(&xch[NL * r + j]) = make_double2(E[r][j], E[r][j + 1]);
-      double sr = s[0], dr = ddr[0];
-#pragma unroll
-      for (int r = 1; r < MR; ++r) {
-        sr = prow == r ? s[r] : sr;
-        dr = prow == r ? ddr[r] : dr;
-      }
-      *reinterpret_cast<double2 *>(&xch[NL * MR]) = make_double2(sr, dr);
-    }
-    wave_lds_sync();
-    const double *xr = xch + (MR > 1 ? NL * prow : 0);
-    const double Dpl = xr[l];
-    const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NL * MR]);
-    const double Dpq = xr[q & (NL - 1)];  // q == 16: an ADD is impossible (d2 = 0)
-#else
     if (l == owner) {
 #pragma unroll
       for (int r = 0; r < MR; ++r)
@@ -422,19 +393,7 @@ __device__ __forceinline__ void gi_group(
     const double Dpl = xch[l];
     const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NL]);
     const double Dpq = xch[q & (NL - 1)];  // q == 16: an ADD is impossible (d2 = 0)
-#endif
     const double sp = spdd.x, dd = spdd.y;  // s_p, |D[p,:]|^2
-#if QPB_RV_PREFETCH
-    // the back substitution's R entries R[l][j], j < min(qmax, RV), issued here
-    double rv[QPB_RV_PREFETCH];
-    unroll<QPB_RV_PREFETCH / 4>([&](auto G) {
-      constexpr int g4 = 4 * G;
-      if (qmax > g4) {
-#pragma unroll
-        for (int j = g4; j < g4 + 4; ++j) rv[j] = Tv[j * NL + l];
-      }
-    });
-#endif
     wave_lds_sync();
     const double d2 = (l >= q) ? Dpl : 0.0;  // D[p, q:]
     dpp_ready(d2);
@@ -454,11 +413,6 @@ __device__ __forceinline__ void gi_group(
       double nacc = (l < q) ? Dpl : 0.0;  // = -d1_l
       unroll<NL>([&](auto JJ) {
         constexpr int j = NL - 1 - JJ;
-#if QPB_RV_PREFETCH
-        if constexpr (j < QPB_RV_PREFETCH) {
-          if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, rv[j]);
-        } else
-#endif
         if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, Tv[j * NL + l]);
       });
       rm = nacc * ninv;  // r_l (0 for l >= q)
