@@ -43,10 +43,6 @@
 #include "qpb_common.h"
 #include "qpb.h"
 
-#ifndef GRAM_BC
-#define GRAM_BC 1
-#endif
-
 namespace qpb {
 namespace gram {
 
@@ -151,7 +147,6 @@ __device__ __forceinline__ double pair16(double v) {
 __device__ __forceinline__ double group_sum(double v) { return pair16(pair32(v)); }
 // this lane's rows of D (one per tile) against a permuted vector in LDS
 __device__ __forceinline__ void row_dot(const double (&E)[RT][8][4], const double *vp, double (&out)[RT]) {
-#if GRAM_BC
   // the 16 lanes of a group need the same 32 entries: lane j reads entries
   // 2j, 2j + 1 (one b128 instead of sixteen), and the FMAs take entry 4k + c
   // from lane 2k + c / 2 by a fused row_newbcast (same products, same order)
@@ -173,27 +168,6 @@ __device__ __forceinline__ void row_dot(const double (&E)[RT][8][4], const doubl
   });
 #pragma unroll
   for (int t = 0; t < RT; ++t) out[t] = group_sum((a[t][0] + a[t][1]) + (a[t][2] + a[t][3]));
-#else
-  double a[RT][4];
-#pragma unroll
-  for (int t = 0; t < RT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a[t][r] = 0.0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const double2 x = *reinterpret_cast<const double2 *>(&vp[4 * k]);
-    const double2 y = *reinterpret_cast<const double2 *>(&vp[4 * k + 2]);
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      a[t][0] = __builtin_fma(E[t][k][0], x.x, a[t][0]);
-      a[t][1] = __builtin_fma(E[t][k][1], x.y, a[t][1]);
-      a[t][2] = __builtin_fma(E[t][k][2], y.x, a[t][2]);
-      a[t][3] = __builtin_fma(E[t][k][3], y.y, a[t][3]);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < RT; ++t) out[t] = group_sum((a[t][0] + a[t][1]) + (a[t][2] + a[t][3]));
-#endif
 }
 // symmetric packed access
 __device__ __forceinline__ double sym(const double *P, int i, int j) { return i >= j ? P[tri(i, j)] : P[tri(j, i)]; }
