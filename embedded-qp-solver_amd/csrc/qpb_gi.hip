@@ -26,8 +26,10 @@
 //           prefetched R column), partial step t1 (ratio test over the active
 //           multipliers), full step t2 = -s_p / |d2|^2, slacks s -= t D d2.
 //           full step  -> ADD p: one Householder reflection on columns q..15
-//                         of D (every lane updates its own rows), new column
-//                         of R;
+//                         of D (every lane updates its own rows; its product
+//                         D v = D d2 + alpha D[:, q] reuses the slack step's
+//                         D d2 and reads column q by a branch tree on q), new
+//                         column of R;
 //           partial    -> DROP k: delete column k of R, Givens rotations
 //                         restore triangularity (also applied to D).
 //   finish  x = -H^{-1} (f + A^T lam) from the final multipliers (KKT
@@ -456,11 +458,24 @@ __device__ __forceinline__ void gi_group(
       const double beta = ir * rcp1(nrm + __builtin_fabs(Dpq));
       const double ia = neg ? -ir : ir;  // 1 / alpha
       const double v = d2 + (l == q ? alpha : 0.0);
-      dpp_ready(v);
+      // E v = E d2 + alpha E[:, q] = u + alpha E[:, q]: no second product;
+      // column q by a branch tree on q (its distinct values in the wave)
       double nw[MR];
-      bdot_rows<MR>(v, E, nw);
+      switch (q & (NL - 1)) {
+#define QPB_COLQ_CASE(J)                                        \
+  case J:                                                        \
+    asm volatile("");                                            \
+    for (int r = 0; r < MR; ++r) nw[r] = E[r][J];                \
+    break;
+        QPB_COLQ_CASE(0) QPB_COLQ_CASE(1) QPB_COLQ_CASE(2) QPB_COLQ_CASE(3)
+        QPB_COLQ_CASE(4) QPB_COLQ_CASE(5) QPB_COLQ_CASE(6) QPB_COLQ_CASE(7)
+        QPB_COLQ_CASE(8) QPB_COLQ_CASE(9) QPB_COLQ_CASE(10) QPB_COLQ_CASE(11)
+        QPB_COLQ_CASE(12) QPB_COLQ_CASE(13) QPB_COLQ_CASE(14) QPB_COLQ_CASE(15)
+#undef QPB_COLQ_CASE
+      }
 #pragma unroll
-      for (int r = 0; r < MR; ++r) nw[r] *= -beta;
+      for (int r = 0; r < MR; ++r) nw[r] = -beta * __builtin_fma(alpha, nw[r], u[r]);
+      dpp_ready(v);
 #pragma unroll
       for (int r = 0; r < MR; ++r) unroll<NL>([&](auto J) {
           constexpr int j = J;

@@ -443,8 +443,26 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       fn2 = __builtin_fmaxf(__builtin_fmaf(-cq, cq, fn2), 0.0f);
       // v = d2 + alpha e_q in the DPP operand pair; E -= beta (E . v) v^T
       const double vA = d2A + (li == q ? alpha : 0.0), vB = d2B + (li + NH == q ? alpha : 0.0);
+      // E v = E d2 + alpha E[:, q] = ud + alpha E[q] (q wave-uniform: a
+      // scalar branch tree picks the register)
+      double eq = 0.0;
+      switch (q & (NP - 1)) {
+#define QPB_COLQ_CASE(J) \
+  case J:                \
+    eq = E[J];           \
+    break;
+        QPB_COLQ_CASE(0) QPB_COLQ_CASE(1) QPB_COLQ_CASE(2) QPB_COLQ_CASE(3)
+        QPB_COLQ_CASE(4) QPB_COLQ_CASE(5) QPB_COLQ_CASE(6) QPB_COLQ_CASE(7)
+        QPB_COLQ_CASE(8) QPB_COLQ_CASE(9) QPB_COLQ_CASE(10) QPB_COLQ_CASE(11)
+        QPB_COLQ_CASE(12) QPB_COLQ_CASE(13) QPB_COLQ_CASE(14) QPB_COLQ_CASE(15)
+        QPB_COLQ_CASE(16) QPB_COLQ_CASE(17) QPB_COLQ_CASE(18) QPB_COLQ_CASE(19)
+        QPB_COLQ_CASE(20) QPB_COLQ_CASE(21) QPB_COLQ_CASE(22) QPB_COLQ_CASE(23)
+        QPB_COLQ_CASE(24) QPB_COLQ_CASE(25) QPB_COLQ_CASE(26) QPB_COLQ_CASE(27)
+        QPB_COLQ_CASE(28) QPB_COLQ_CASE(29) QPB_COLQ_CASE(30) QPB_COLQ_CASE(31)
+#undef QPB_COLQ_CASE
+      }
+      const double mw = -beta * __builtin_fma(alpha, eq, ud);
       dpp_ready2(vA, vB);
-      const double mw = -beta * bdot(E, vA, vB);
       unroll<NH>([&](auto J) {
         constexpr int j = J;
         fmac_bc<j>(E[j], vA, mw);

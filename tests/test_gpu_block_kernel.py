@@ -61,7 +61,8 @@ def test_block_kernel_unconstrained(qpb):
 @pytest.mark.parametrize("kind", ["box", "dense"])
 def test_config3_full_batch(qpb, kind):
     """BASELINE configs[3] as specified (n=128, m=256, B=16384) from the
-    on-device generator: every QP KKT-certified, 32 QPs against the oracle."""
+    on-device generator: every QP KKT-certified, 128 QPs spread over the batch
+    against the oracle (x, mask)."""
     B = 16384
     H, f, A, b = qpb.generate(128, B, 20261015, family=kind)
     sol = qpb.solve(H, f, A, b)
@@ -75,7 +76,7 @@ def test_config3_full_batch(qpb, kind):
         Hn, fn, An, bn = (t[sl].cpu().numpy() for t in (H, f, A, b))
         r = O.kkt_residuals(Hn, fn, An, bn, x[sl], lam[sl])
         assert max(float(v.max()) for v in r.values()) <= 1e-9, (k0, {k: float(v.max()) for k, v in r.items()})
-    idx = np.linspace(0, B - 1, 32).astype(int)
+    idx = np.linspace(0, B - 1, 128).astype(int)
     Hn, fn, An, bn = (t[idx].cpu().numpy() for t in (H, f, A, b))
     for j, i in enumerate(idx):
         ref = O.active_set_solve(Hn[j], fn[j], An[j], bn[j])

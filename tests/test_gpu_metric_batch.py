@@ -60,7 +60,7 @@ def test_metric_batch_1m(qpb, family):
     mask = bits.reshape(B, -1)[:, :32].bool()
     assert float((mask == (sol.lam > 0)).double().mean()) > 0.9999
     # independent primal oracle on a sample spread over the batch
-    idx = np.random.default_rng(1).choice(B, size=48, replace=False)
+    idx = np.random.default_rng(1).choice(B, size=1022, replace=False)
     idx = np.concatenate([idx, [0, B - 1]])
     Hs, fs, As, bs = (t[idx].cpu().numpy() for t in (H, f, A, b))
     xs, ms = sol.x[idx].cpu().numpy(), mask[idx].cpu().numpy()
