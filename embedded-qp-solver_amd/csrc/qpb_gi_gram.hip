@@ -692,12 +692,28 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       // over the columns li + 16 i (row sums over the 16 lanes finish it)
       for (int t0 = 4 * wv; t0 < q; t0 += 4 * NWV) {
         const int t = t0 + lk;
-        const double *qr = QR.row(t < q ? t : t0);
+        const int tt = t < q ? t : t0;
+        // all eight Q1 entries and u entries in flight before the FMAs; rows
+        // in LDS (the usual case, wave-uniform test) are read as LDS, not
+        // through generic pointers (flat loads, each waited for)
+        double qv[8], uv[8];
+        if (t0 + 3 < QL) {
+          const __attribute__((address_space(3))) double *qr =
+              (const __attribute__((address_space(3))) double *)(QR.lds + tt * QS);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) qv[i] = qr[li + 16 * i];
+        } else {
+          const double *qr = QR.row(tt);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) qv[i] = qr[li + 16 * i];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) uv[i] = ub[pad(li + 16 * i)];
         double a0 = 0.0, a1 = 0.0;
 #pragma unroll
         for (int i = 0; i < 8; i += 2) {
-          a0 = __builtin_fma(qr[li + 16 * i], ub[pad(li + 16 * i)], a0);
-          a1 = __builtin_fma(qr[li + 16 * i + 16], ub[pad(li + 16 * i + 16)], a1);
+          a0 = __builtin_fma(qv[i], uv[i], a0);
+          a1 = __builtin_fma(qv[i + 1], uv[i + 1], a1);
         }
         const double dv = row_sum(a0 + a1);
         if (li == 0 && t < q) db[t] = dv;
@@ -711,6 +727,16 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         double acc0 = 0.0, acc1 = 0.0;
         const int qa = q < QL ? q : QL;
         int j = lk;
+        // four positions per step, their eight reads in flight together
+        for (; j + 12 < qa; j += 16) {
+          const double d0 = db[j], d1 = db[j + 4], d2 = db[j + 8], d3 = db[j + 12];
+          const double q0 = QR.lds[j * QS + c], q1 = QR.lds[(j + 4) * QS + c];
+          const double q2 = QR.lds[(j + 8) * QS + c], q3 = QR.lds[(j + 12) * QS + c];
+          acc0 = __builtin_fma(d0, q0, acc0);
+          acc1 = __builtin_fma(d1, q1, acc1);
+          acc0 = __builtin_fma(d2, q2, acc0);
+          acc1 = __builtin_fma(d3, q3, acc1);
+        }
         for (; j + 4 < qa; j += 8) {
           acc0 = __builtin_fma(db[j], QR.lds[j * QS + c], acc0);
           acc1 = __builtin_fma(db[j + 4], QR.lds[(j + 4) * QS + c], acc1);
@@ -729,10 +755,19 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         const int i = 16 * wv + li;
         double ratio = kBig;
         if (16 * wv < q) {
-          double acc = 0.0;
+          double acc = 0.0, acc1 = 0.0;
           int c = lk + ((i > lk) ? ((i - lk + 3) & ~3) : 0);
+          // four columns per step, their eight reads in flight together
+          for (; c + 12 < q; c += 16) {
+            const double z0 = Lp[tri(c, i)], z1 = Lp[tri(c + 4, i)], z2 = Lp[tri(c + 8, i)], z3 = Lp[tri(c + 12, i)];
+            const double d0 = db[c], d1 = db[c + 4], d2 = db[c + 8], d3 = db[c + 12];
+            acc = __builtin_fma(z0, d0, acc);
+            acc1 = __builtin_fma(z1, d1, acc1);
+            acc = __builtin_fma(z2, d2, acc);
+            acc1 = __builtin_fma(z3, d3, acc1);
+          }
           for (; c < q; c += 4) acc = __builtin_fma(Lp[tri(c, i)], db[c], acc);
-          const double rt = group_sum(acc);
+          const double rt = group_sum(acc + acc1);
           if (i < q) {
             if (lk == 0) rb[i] = rt;
             if (rt > 0.0) ratio = lamb[i] * rcp(rt);

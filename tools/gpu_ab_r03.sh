@@ -2,7 +2,7 @@
 # round-3 A/B session: parity of each candidate, then interleaved kernel timing
 # (n=16 dense kernel at 1M box + dense, box fast path, n=32 wave kernel)
 cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out/ab || exit 1
-DV=${DV:-vB}; BV=${BV:-bB}; WV=${WV:-wB}
+DV=${DV-vB}; BV=${BV-bB}; WV=${WV-wB}
 for v in $DV; do
   QPB_LIB=embedded-qp-solver_amd/lib/libqpb_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_active_set.py tests/test_gpu_metric_batch.py -x -q --timeout 250 --timeout-method thread > gpurun_out/ab/pytest_$v.log 2>&1 || { tail -20 gpurun_out/ab/pytest_$v.log; exit 1; }
   echo "pytest $v: $(tail -1 gpurun_out/ab/pytest_$v.log)"
