@@ -258,18 +258,20 @@ __device__ __forceinline__ void gi_group(
   // broadcast) = column k by symmetry, so L[j][k] = pr[j] / sqrt(akk) and
   //   row l:  Lr[j] -= c pr[j] (j > k),  c = Lr[k] / akk;   Lr[k] = L[l][k]
   //   D rows: E[k] /= sqrt(akk), E[j] -= E[k] pr[j] / akk (j > k)
-  //   y:      lane-parallel, f_l -= c f_k;  y_k = f_k / sqrt(akk)
+  //   y:      lane-parallel, f_l -= c f_k (f_k read from lane k by the FMA)
   // Lanes l < k keep updating dead entries of their row (the upper triangle,
   // never read).  The pivot row is read straight from lane k by the FMAs
   // (v_fmac_f64_dpp); the sched_barrier and the rsq chain keep every write of
-  // Lr[j] (previous step) well over two instructions before these reads.
-  // Lane k's own Lr[j] is updated last, after the D rows have read it.
-  // s = b + D y accumulates in the same sweep (D[:, k] and y_k are final at
-  // step k).
+  // Lr[j] and of f (previous step) well over two instructions before these
+  // reads.  Lane k's own Lr[j] is updated last, after the D rows have read it.
+  // s = b + D y accumulates in the same sweep, negated: D[r][k] y_k =
+  // (e ik)(f_k ik) = -ne2 f_k, one DPP-fused FMA per row with f_k from lane k
+  // (y itself is never formed).
   bool spd = true;
   double ya = fl;
+  double ns[MR];  // -s during the sweep
 #pragma unroll
-  for (int r = 0; r < MR; ++r) s[r] = bl[r];
+  for (int r = 0; r < MR; ++r) ns[r] = -bl[r];
   unroll<NL>([&](auto K) {
     constexpr int k = K;
     __builtin_amdgcn_sched_barrier(0);
@@ -285,21 +287,20 @@ __device__ __forceinline__ void gi_group(
       ne2[r] = -(e * ik2);
       E[r][k] = e * ik;
     }
+#pragma unroll
+    for (int r = 0; r < MR; ++r) fmac_bc<k>(ns[r], ya, ne2[r]);
     unroll<NL - 1 - k>([&](auto J) {
       constexpr int j = k + 1 + J;
 #pragma unroll
       for (int r = 0; r < MR; ++r) fmac_bc<k>(E[r][j], Lr[j], ne2[r]);
       fmac_bc<k>(Lr[j], Lr[j], nc);
     });
+    fmac_bc<k>(ya, ya, nc);  // lane k's own f_k becomes 0 (dead)
     Lr[k] *= ik;
-    const double c = -nc;
-    const double fk = bc<k>(ya);
-    ya = __builtin_fma(-c, fk, ya);
-    const double yk = fk * ik;  // y_k; D[r][k] is final now
-#pragma unroll
-    for (int r = 0; r < MR; ++r) s[r] = __builtin_fma(E[r][k], yk, s[r]);
   });
   __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = 0; r < MR; ++r) s[r] = -ns[r];
   // L -> LDS, packed rows (lane l writes row l), kept for the final solves.
   // Lane l also writes its dead entries j > l, over the start of later rows:
   // stores go in descending j, and a row's own entry at such an address has

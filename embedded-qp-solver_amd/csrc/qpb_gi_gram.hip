@@ -67,7 +67,7 @@ constexpr int QL = (OFF_BUF - OFF_ROWS) / QS;  // Q1 rows in LDS (70)
 constexpr int B_CAND = OFF_BUF;                // per wave: its most violated row of D (PV each)
 constexpr int B_CSP = B_CAND + NWV * PV;       // per wave: that row's slack
 constexpr int B_W = B_CSP + NWV;               // w (padded permuted)
-constexpr int B_V = B_W + PV;                  // DROP scratch (row k of Z); lambda scatter at the end
+constexpr int B_V = B_W + PV;                  // per-wave candidate row norms (NWV) and DROP scratch (row k of Z, at NB); lambda scatter at the end
 constexpr int B_R = B_V + MB;                  // r by position
 constexpr int B_CB = B_R + NB;                 // d = Q1 u by position
 constexpr int B_LAM = B_CB + NB;               // multipliers by position
@@ -569,6 +569,21 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       }
     }
     clk.tick(1);
+    // |D[row,:]|^2 of the lane's rows (the dependency test's scale, published
+    // with the selection key: no |u|^2 reduction in the loop)
+    double dn2[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a0 = __builtin_fma(E[t][k][0], E[t][k][0], a0);
+        a1 = __builtin_fma(E[t][k][1], E[t][k][1], a1);
+        a0 = __builtin_fma(E[t][k][2], E[t][k][2], a0);
+        a1 = __builtin_fma(E[t][k][3], E[t][k][3], a1);
+      }
+      dn2[t] = group_sum(a0 + a1);
+    }
     double invn[RT], thr[RT], s[RT];
     bool zero_bad = false, act[RT];
 #pragma unroll
@@ -647,7 +662,10 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       if (key < kBig) {
 #pragma unroll
         for (int t = 0; t < RT; ++t)
-          if (row[t] == pw && lk == 0) lds[B_CSP + wv] = s[t];
+          if (row[t] == pw && lk == 0) {
+            lds[B_CSP + wv] = s[t];
+            vb[wv] = dn2[t];  // B_V is free during the loop below NB
+          }
       }
     };
     if (tid < NB) {
@@ -683,9 +701,8 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
             }
         }
         __syncthreads();
-        // |u|^2 (the dependency test's scale) on every wave
-        const double ua = ub[pad(l)], ubb = ub[pad(l + 64)];
-        dd = wave_sum(__builtin_fma(ua, ua, ubb * ubb));
+        // |u|^2 (the dependency test's scale), published with the key
+        dd = vb[p / (16 * RT)];
       }
       clk.tick(3);
       // ---- d = Q1 u: lane (lk, li) of wave w takes position 32 j + 4 w + lk
