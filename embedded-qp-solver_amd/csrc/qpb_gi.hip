@@ -588,42 +588,67 @@ __device__ __forceinline__ void gi_group(
   clk.tick(10);
 
   // ------------------------------------------------------------- outputs
-  // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iam_k} (the active rows of
-  // A re-read, one coalesced 128-B row per active position), then L y = g,
-  // L^T x = -y, lane-parallel: step k broadcasts the finished component from
-  // lane k; finished lanes keep updating (dead values) and the components are
-  // captured by same-address LDS stores.
+  // (the active rows of A re-read, one coalesced 128-B row per active position)
   const int qm = __builtin_elementwise_min(wave_max4(q), NL);
-  double gl = fl;
-  {
-    // all loads first (branch-free: inactive positions read row 0 and carry
-    // a zero multiplier), then the sum
-    const int ias = iam > 0 ? iam : 0;
-    const int lc = l < n ? l : n - 1;
-    unroll<2>([&](auto H) {
-      constexpr int k0 = 8 * H;
-      // one wave-uniform test per group of eight: a test per load made each
-      // load of the second group a branch with its own wait (eight serial
-      // round trips); positions past qm read a valid row and are not summed
-      if (k0 < qm) {
-        double arow[8];
-        __builtin_amdgcn_sched_barrier(0);
-        unroll<8>([&](auto K) {
-          constexpr int kk = k0 + K;
-          arow[K] = Aq[bci<kk>(ias) * n + lc];
-        });
-        unroll<8>([&](auto K) {
-          constexpr int kk = k0 + K;
-          if (kk < qm) gl = __builtin_fma(bc<kk>(um), (N16 || l < n) ? arow[K] : 0.0, gl);
-        });
-      }
-    });
-  }
+  // The A-row loads go out first, in at most two groups of eight (one
+  // wave-uniform test per group: a test per load made each load a branch
+  // with its own wait); the work that does not need them -- the multipliers by
+  // row and their stores, the active-set word, L's row -- runs while they are
+  // in flight.  Positions past qm read a valid row and are not summed.
+  const int ias = iam > 0 ? iam : 0;
+  asm volatile("s_nop 1" ::"v"(ias));  // its DPP reads below may sit behind a branch only
+  const int lc = l < n ? l : n - 1;
+  double arow[NL];
+  unroll<2>([&](auto H) {
+    constexpr int k0 = 8 * H;
+    if (k0 < qm) {
+      __builtin_amdgcn_sched_barrier(0);
+      unroll<8>([&](auto K) {
+        constexpr int kk = k0 + K;
+        arow[kk] = Aq[bci<kk>(ias) * n + lc];
+      });
+    }
+  });
+  double *lamb = xch;  // lambda scatter (32); the solves below reuse xch afterwards
+#pragma unroll
+  for (int r = 0; r < 2; ++r) lamb[l + NL * r] = 0.0;
+  wave_lds_sync();
+  if (l < q && iam >= 0) lamb[iam] = um;
+  wave_lds_sync();
+  double lamr[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) lamr[r] = lamb[l + NL * r];
   const double invd = rcp1(Lp[lrow(l) + l]);
   double Lrow[NL];  // row l of L (entries past l are dead)
 #pragma unroll
   for (int j = 0; j < NL; ++j) Lrow[j] = Lp[lrow(l) + j];
   wave_lds_sync();
+#pragma unroll
+  for (int r = 0; r < MR; ++r) {
+    const int row = l + NL * r;
+    if (live && (FULL || row < m)) lamg[g * m + row] = lamr[r];
+  }
+  uint32_t w0 = 0;
+#pragma unroll
+  for (int r = 0; r < MR; ++r) {
+    const unsigned long long bal = __ballot(act[r]);
+    w0 |= (uint32_t)((bal >> sh) & 0xFFFFull) << (16 * r);
+  }
+  if (live && l == 0 && m > 0) actg[g] = w0;
+  // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iam_k}, then L y = g,
+  // L^T x = -y, lane-parallel: step k broadcasts the finished component from
+  // lane k; finished lanes keep updating (dead values) and the components are
+  // captured by same-address LDS stores.
+  double gl = fl;
+  unroll<2>([&](auto H) {
+    constexpr int k0 = 8 * H;
+    if (k0 < qm) {
+      unroll<8>([&](auto K) {
+        constexpr int kk = k0 + K;
+        if (kk < qm) gl = __builtin_fma(bc<kk>(um), (N16 || l < n) ? arow[kk] : 0.0, gl);
+      });
+    }
+  });
   {
     double acc = gl;
     unroll<NL>([&](auto K) {
@@ -646,32 +671,13 @@ __device__ __forceinline__ void gi_group(
   }
   wave_lds_sync();
   const double xl = -xch[l];
-  double *lamb = xch;  // lambda scatter (32), after x is read
-  wave_lds_sync();
   {
     // a non-finite x on any lane -> NUMERICAL for the QP
     const double bad = row_min((__builtin_fabs(xl) < kInf) ? 0.0 : -1.0);
     if (status == QPB_OK && bad < 0.0) status = QPB_NUMERICAL;
   }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) lamb[l + NL * r] = 0.0;
-  wave_lds_sync();
-  if (l < q && iam >= 0) lamb[iam] = um;
-  wave_lds_sync();
-#pragma unroll
-  for (int r = 0; r < MR; ++r) {
-    const int row = l + NL * r;
-    if (live && (FULL || row < m)) lamg[g * m + row] = lamb[row];
-  }
   if (live && (N16 || l < n)) xg[g * n + l] = xl;
-  uint32_t w0 = 0;
-#pragma unroll
-  for (int r = 0; r < MR; ++r) {
-    const unsigned long long bal = __ballot(act[r]);
-    w0 |= (uint32_t)((bal >> sh) & 0xFFFFull) << (16 * r);
-  }
   if (live && l == 0) {
-    if (m > 0) actg[g] = w0;
     statg[g] = status;
     if (itg) itg[g] = it;
   }
