@@ -35,7 +35,7 @@ def t_kernel(fn, reps=15):
 def _diag_args(H, f, A, b, sol, flags=1):
     import ctypes
     B, n = f.shape
-    d = qpb.Desc(n, A.shape[1], B, 0, flags, 0.0)  # 1 = QPB_FLAG_DIAG_L2, 4 = QPB_FLAG_DIAG_OCC2, 8 = persistent
+    d = qpb.Desc(n, A.shape[1], B, 0, flags, 0.0)  # 1 = QPB_FLAG_DIAG_L2, 16 = QPB_FLAG_DIAG_MALL
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     return (ctypes.byref(d), p(H), p(f), p(A), p(b), p(sol.x), p(sol.lam), p(sol.active), p(sol.status),
             p(sol.iters), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
