@@ -171,6 +171,11 @@ def cpu_run(fn: str, iters: int, H, f, seconds: float, procs: int, lib_name: str
     import multiprocessing as mp
 
     import numpy as np
+    torch_mod = sys.modules.get("torch")
+    if torch_mod is not None and torch_mod.cuda.is_initialized():
+        # forked workers would inherit the HIP runtime state (and a profiler's
+        # signal handlers): the config sweep's SIGSEGV of round 3
+        raise RuntimeError("bench.cpu_run: the GPU is initialised in this process; run the CPU leg first")
     lib = os.path.join(ROOT, "oracle", "_ref", lib_name)
     if not os.path.exists(lib):
         return None
@@ -231,7 +236,7 @@ def main():
                     help="total QPs sharded over the GPUs (strong scaling; default: the metric's 1M)")
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (weak scaling; overrides --global-batch)")
     ap.add_argument("--gather", action="store_true",
-                    help="after the timed region, all-gather x/lam/active/status over RCCL and time it")
+                    help="after the timed region, gather x/lam/active/status to rank 0 over RCCL and time it")
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--family", choices=["box", "dense"], default="box")
     ap.add_argument("--seed", type=int, default=20261015)
@@ -240,6 +245,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=4096)
     ap.add_argument("--ref-batch", type=int, default=65536, help="QPs for the GPU Newton/ADMM replica rows")
     ap.add_argument("--box-reps", type=int, default=10, help="timed qpb_solve_box calls on the same QPs (0: skip)")
+    ap.add_argument("--dense-reps", type=int, default=10, help="timed qpb_solve calls on the dense family (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify statuses after the timed region")
     args = ap.parse_args()
@@ -330,13 +336,19 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(e) for a, e in evs) / args.steps
     elapsed = max_over_ranks(elapsed, device)
-    gather_ms = None
+    gather_ms, gather = None, None
     if args.gather and world > 1:  # the trivial result gather of SURVEY.md §8e, outside the timed steps
         barrier()
         tg = time.perf_counter()
         full = gather_results({"x": sol.x, "lam": sol.lam, "active": sol.active, "status": sol.status}, total_B)
         barrier()
         gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, device)
+        if rank == 0:
+            # rank 0 holds the whole batch: its own shard in place, every status a valid code
+            checked = bool(full["x"].shape[0] == total_B and torch.equal(full["x"][start:start + B], sol.x)
+                           and ((full["status"] >= 0) & (full["status"] <= 4)).all())
+            gather = {"dst": 0, "collective": "gather (x, lam, active, status) to rank 0",
+                      "bytes_per_qp": 8 * (n + m) + 4 * ((m + 31) // 32) + 4, "checked": checked}
         del full
 
     st = sol.status.cpu()
@@ -390,6 +402,30 @@ def main():
                "ok_frac": float((bsol.status == 0).double().mean())}
         del bsol
 
+    # the dense family (random normalised A rows) at the same
+    # batch: the same kernel on QPs whose constraints are not a box in disguise
+    dense = None
+    if rank == 0 and world == 1 and n <= 16 and args.family == "box" and args.dense_reps > 0:
+        Hd, fd, Ad, bd = qpb.generate(n, B, args.seed, family="dense", shift=1.0, box=10.0, device=device)
+        dsol = qpb.solve(Hd, fd, Ad, bd, stream=stream)
+        dev_ = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.dense_reps)]
+        torch.cuda.synchronize()
+        for e0, e1 in dev_:
+            e0.record(stream)
+            qpb.solve(Hd, fd, Ad, bd, out=dsol, stream=stream)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        dense_ms = sum(a.elapsed_time(e) for a, e in dev_) / len(dev_)
+        dbytes = bytes_per_qp(n, m)
+        dit = dsol.iters.double()
+        dense = {"family": "dense (A rows ~ N(0, I) normalised, b ~ U[0.1, 1) * 10)", "qps_per_s": B / (dense_ms * 1e-3),
+                 "kernel_ms": dense_ms, "bytes_per_qp": dbytes,
+                 "hbm_frac": B * dbytes / (dense_ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
+                 "ok_frac": float((dsol.status == 0).double().mean()), "iters_mean": float(dit.mean()),
+                 "iters_max": int(dit.max())}
+        del Hd, fd, Ad, bd, dsol
+
     total_qps = total_B * args.steps
     value = total_qps / elapsed
     bpq = bytes_per_qp(n, m)
@@ -430,6 +466,8 @@ def main():
             "box_fast_path": box,
             "solver_stats": {"ok_frac": ok_frac, "iters_mean": float(it.mean()), "iters_max": int(it.max())},
             "gather_ms": gather_ms,
+            "gather": gather,
+            "dense_family": dense,
             "distributed": dist_info,
             "library": qpb.version(),
         }

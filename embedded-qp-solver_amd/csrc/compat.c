@@ -81,8 +81,18 @@ static void pool_release(void)
 
 void qpb_compat_init(unsigned n_dim, double admm_box_min, double admm_box_max)
 {
-	if (n_dim == 0 || n_dim > 65535)
-		n_dim = 48;
+	/* The reference packs N_DIM into 16 bits (matrix_type.h:14-17), but its
+	 * solvers run here on the GPU replicas (qpb_ref_solve), which take
+	 * n <= QPB_MAX_N: refuse such an N_DIM now, with the reason, instead of
+	 * failing inside the caller's first solve. */
+	if (n_dim == 0 || n_dim > QPB_MAX_N) {
+		fprintf(stderr,
+			"kmalloc_init: N_DIM = %u is outside 1..%d: the qp_solvers.h solvers of this library "
+			"(gradient_descent_with_line_search, newton_method_with_line_search, admm) run on the "
+			"batched GPU replicas, which take n <= %d (qpb.h QPB_MAX_N)\n",
+			n_dim, QPB_MAX_N, QPB_MAX_N);
+		exit(EXIT_FAILURE);
+	}
 	pool_release();
 	g_ndim = n_dim;
 	g_box_min = admm_box_min;

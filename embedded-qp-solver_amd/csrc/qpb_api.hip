@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include "qpb.h"
+#include "qpb_common.h"  // kSectionSlots, kSections
 
 extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const double *f, const double *A,
                                     const double *b, double *x, double *lam, uint32_t *active,
@@ -166,9 +167,13 @@ extern "C" int qpb_solve_box(const qpb_desc *d, const double *H, const double *f
 
 extern "C" int qpb_solve_sections(const qpb_desc *d, const double *H, const double *f, const double *A,
                                   const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
-                                  int32_t *iters, unsigned long long *sections, void *stream) {
+                                  int32_t *iters, unsigned long long *sections, int64_t sections_len,
+                                  void *stream) {
   int rc = check_desc(d);
   if (rc) return rc;
+  static_assert(QPB_SECTIONS_LEN == qpb::kSectionSlots * qpb::kSections, "sections buffer shape");
+  if (sections && sections_len < QPB_SECTIONS_LEN)
+    return fail(QPB_ERR_INVALID_ARG, "sections: the buffer must hold QPB_SECTIONS_LEN (256 x 20) counters");
   if (d->batch == 0) return 0;
   const bool n16 = d->n == 16 && d->m > 16 && d->m <= 32, wave = d->n > 16 && d->n <= 32 && d->m <= 64;
   const bool gram = !(d->n <= 32 && d->m <= 64) && d->batch <= chunk_qps(d->n, d->m);

@@ -14,7 +14,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <utility>
+
+// Cached per-(device, stream) device scratch (qpb_workspace.hip): `launch`
+// receives the buffer (>= bytes) and queues its work on `stream` while the
+// cache is locked, so no other thread can grow (free) it in between.
+hipError_t qpb_with_workspace(hipStream_t stream, size_t bytes, const std::function<hipError_t(void *)> &launch)
+    __attribute__((visibility("hidden")));
 
 namespace qpb {
 

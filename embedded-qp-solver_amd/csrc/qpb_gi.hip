@@ -72,6 +72,12 @@ constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: exchange rows (MR x 16), s_p, 
                                           // cos / sin (16 + 16); y / x capture; lambda scatter
 constexpr int SLOT = OFF_XCH + 34;        // 426 (4 x 426 x 8 B = 13,632 B per wave: 12 waves per CU)
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
+// n == 16: D = A L^{-T} on the fp64 matrix cores (v_mfma_f64_4x4x4_4b_f64) by
+// blocked forward substitution; the VALU sweep factorises H only
+#ifndef QPB_GI_MFMA
+#define QPB_GI_MFMA 1
+#endif
+constexpr int OFF_Y = 104;  // (y_k, 1/L_kk) captures of the sweep (inside L's area, written after)
 static_assert(SLOT % 2 == 0 && OFF_T % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
 static_assert(4 * SLOT * 8 <= 160 * 1024 / 12, "12 waves (3 per SIMD) per CU by LDS");
 static_assert(NL * RS <= SLOT - OFF_T, "input transposes are staged in T + xch");
@@ -114,6 +120,34 @@ __device__ __forceinline__ void bdot_rows(double vec, const double (&x)[MR][NL],
 #pragma unroll
   for (int r = 0; r < MR; ++r) out[r] = a[r][0] + a[r][1];
 }
+
+// v_mfma_f64_4x4x4_4b_f64 (tools/probe/mfma44_probe.hip): block b = lane bits
+// 2-3; A(i,k) at lane i + 4b + 16k, B(k,j) at j + 4b + 16k, C(i,j) at
+// j + 4b + 16i.  Block b carries QP b, whose operands come from slot b's LDS.
+__device__ __forceinline__ double mfma44(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// D = A L^{-T} for one 16-row half of A on the matrix cores, as blocked
+// forward substitution in the transposed form (every tile in the C layout of
+// its transpose, so a product feeds the next one with no data movement):
+//   D_K^T = Linv_K X_K^T,   X_J^T -= L_JK D_K^T  (J > K)
+// Xt[K][i]: lane (row k, block b, c) holds X_b(4i + c, 4K + k) of the half;
+// Ln[J][K]: lane (k, b, i) holds -L_b(4J + i, 4K + k) (A layout);
+// Li[K]: lane (k, b, i) holds inv(L_b[KK])(i, k).  On return Xt holds D.
+__device__ __forceinline__ void mfma_fwd_subst(double (&Xt)[4][4], const double (&Ln)[4][4], const double (&Li)[4]) {
+  unroll<4>([&](auto KK) {
+    constexpr int K = KK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Xt[K][i] = mfma44(Li[K], Xt[K][i], 0.0);
+    unroll<3 - K>([&](auto JJ) {
+      constexpr int J = K + 1 + JJ;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Xt[J][i] = mfma44(Ln[J][K], Xt[K][i], Xt[J][i]);
+    });
+  });
+}
+
 // MR: rows of D per lane (m <= 16 MR).  N16: n == 16 (coalesced loads).
 // FULL: n == 16 and m == 16 MR (no padding rows: no masking anywhere).
 // One group = the 4 QPs of a wavefront; `grp` its index.
@@ -164,7 +198,7 @@ __device__ __forceinline__ void gi_group(
   double Lr[NL];  // row l of H, becomes row l of L
   double E[MR][NL];
   double s[MR], bl[MR], thr[MR];
-  float ddr[MR];  // |D[r,:]|^2 (the dependency test's scale)
+  float ddr[MR];  // |D[r,:]|^2 (the dependency test's scale; clamped to FLT_MAX)
   float fn2[MR];  // |D[r, q:]|^2, the free part of the row (scale of the selection key)
   bool act[MR];
   bool infeasible_row = false;
@@ -173,36 +207,49 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
   for (int r = 0; r < MR; ++r) bv[r] = bq[(FULL || l + NL * r < m) ? l + NL * r : 0];
   const double fv = fg[gi * n + (l < n ? l : n - 1)];
+  const double fl = (N16 || l < n) ? fv : 0.0;
+  constexpr bool kMfma = N16 && QPB_GI_MFMA;
+  [[maybe_unused]] double2 av[MR][8];  // A as loaded (n == 16)
+  [[maybe_unused]] const int hr = l >> 3, hc = 2 * (l & 7);
+  // stage 16 rows of a 16-column matrix (as loaded) in this QP's T region
+  auto stage = [&](const double2 (&v)[8]) {
+    wave_lds_sync();
+#pragma unroll
+    for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&Tv[(2 * t + hr) * RS + hc]) = v[t];
+    wave_lds_sync();
+  };
+  // row r's constant data from its entries: the violation threshold of the
+  // slack, s / |a| < -tol (1 + |b| / |a|), i.e. s < -tol (|a| + |b|) (-inf: a
+  // zero row, never selected), and the zero row's own test 0 <= b
+  auto row_norms = [&](int r, const double (&row)[NL]) {
+    const double nrm2 = dot2<NL>([&](int j) { return row[j]; }, [&](int j) { return row[j]; });
+    const bool ok = FULL || l + NL * r < m;
+    bl[r] = ok ? bv[r] : 0.0;
+    thr[r] = nrm2 > 0.0 ? -feas_tol * (nrm2 * rsq1(nrm2) + __builtin_fabs(bl[r])) : -kInf;
+    infeasible_row = infeasible_row || (ok && nrm2 == 0.0 && bl[r] < -feas_tol * (1.0 + __builtin_fabs(bl[r])));
+    act[r] = false;
+  };
   if constexpr (N16) {
     // Coalesced 16-byte loads: one instruction reads 2 whole rows (256 B) of
     // each of the wave's 4 QPs -- lane l gets row 2t + (l>>3), columns
     // 2(l&7), 2(l&7)+1.  Rows reach their owner lane through a transpose in
     // this QP's T region of LDS (free until the active-set loop).
-    const int hr = l >> 3, hc = 2 * (l & 7);
     double2 hv[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) hv[t] = *reinterpret_cast<const double2 *>(&Hq[(2 * t + hr) * NL + hc]);
-    auto load_a = [&](int r, double2 (&av)[8]) {
+    auto load_a = [&](int r, double2 (&v)[8]) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int row = NL * r + 2 * t + hr;
         if constexpr (FULL)
-          av[t] = *reinterpret_cast<const double2 *>(&Aq[row * NL + hc]);
+          v[t] = *reinterpret_cast<const double2 *>(&Aq[row * NL + hc]);
         else
-          av[t] = row < m ? *reinterpret_cast<const double2 *>(&Aq[row * NL + hc]) : make_double2(0.0, 0.0);
+          v[t] = row < m ? *reinterpret_cast<const double2 *>(&Aq[row * NL + hc]) : make_double2(0.0, 0.0);
       }
-    };
-    auto transpose = [&](const double2 (&v)[8], double (&dst)[NL]) {
-      wave_lds_sync();
-#pragma unroll
-      for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&Tv[(2 * t + hr) * RS + hc]) = v[t];
-      wave_lds_sync();
-      lds_row16(&Tv[l * RS], dst);
     };
     // all input rows in flight at once (one HBM round trip); instruction
     // selection sinks loads to their first use, so an empty asm consumes
     // them right here
-    double2 av[MR][8];
 #pragma unroll
     for (int r = 0; r < MR; ++r) load_a(r, av[r]);
 #pragma unroll
@@ -214,9 +261,22 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
       for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(av[r][t].x), "v"(av[r][t].y));
     }
-    transpose(hv, Lr);
+    stage(hv);
+    lds_row16(&Tv[l * RS], Lr);
+    if constexpr (kMfma) {
+      // the first half of A waits in LDS through the sweep (its row norms now)
+      stage(av[0]);
+      double row[NL];
+      lds_row16(&Tv[l * RS], row);
+      row_norms(0, row);
+    } else {
 #pragma unroll
-    for (int r = 0; r < MR; ++r) transpose(av[r], E[r]);
+      for (int r = 0; r < MR; ++r) {
+        stage(av[r]);
+        lds_row16(&Tv[l * RS], E[r]);
+        row_norms(r, E[r]);
+      }
+    }
     wave_lds_sync();
   } else {  // padded n < 16: clamped per-lane row loads, identity outside n
     const int lc = l < n ? l : n - 1;
@@ -235,86 +295,190 @@ __device__ __forceinline__ void gi_group(
         const double a = Aq[rc * n + (j < n ? j : n - 1)];
         E[r][j] = (ok && j < n) ? a : 0.0;
       }
+      row_norms(r, E[r]);
     }
   }
-#pragma unroll
-  for (int r = 0; r < MR; ++r) {
-    const int row = l + NL * r;
-    const bool ok = FULL || row < m;
-    const double nrm2 = dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
-    bl[r] = ok ? bv[r] : 0.0;
-    // violation threshold of the slack: s / |a| < -tol (1 + |b| / |a|), i.e.
-    // s < -tol (|a| + |b|)  (-inf: zero row, never selected)
-    thr[r] = nrm2 > 0.0 ? -feas_tol * (nrm2 * rsq1(nrm2) + __builtin_fabs(bl[r])) : -kInf;
-    // a zero row is the constant constraint 0 <= b
-    infeasible_row = infeasible_row || (ok && nrm2 == 0.0 && bl[r] < -feas_tol * (1.0 + __builtin_fabs(bl[r])));
-    act[r] = false;
-  }
-  const double fl = (N16 || l < n) ? fv : 0.0;
   clk.tick(0);
 
-  // ---- H = L L^T, D = A L^{-T}, y = L^{-1} f: one right-looking sweep.
-  // Step k: pr = row k of the current Schur complement (lane k's Lr, DPP
-  // broadcast) = column k by symmetry, so L[j][k] = pr[j] / sqrt(akk) and
-  //   row l:  Lr[j] -= c pr[j] (j > k),  c = Lr[k] / akk;   Lr[k] = L[l][k]
-  //   D rows: E[k] /= sqrt(akk), E[j] -= E[k] pr[j] / akk (j > k)
-  //   y:      lane-parallel, f_l -= c f_k (f_k read from lane k by the FMA)
-  // Lanes l < k keep updating dead entries of their row (the upper triangle,
-  // never read).  The pivot row is read straight from lane k by the FMAs
-  // (v_fmac_f64_dpp); the sched_barrier and the rsq chain keep every write of
-  // Lr[j] and of f (previous step) well over two instructions before these
-  // reads.  Lane k's own Lr[j] is updated last, after the D rows have read it.
-  // s = b + D y accumulates in the same sweep, negated: D[r][k] y_k =
-  // (e ik)(f_k ik) = -ne2 f_k, one DPP-fused FMA per row with f_k from lane k
-  // (y itself is never formed).
   bool spd = true;
   double ya = fl;
-  double ns[MR];  // -s during the sweep
-#pragma unroll
-  for (int r = 0; r < MR; ++r) ns[r] = -bl[r];
-  unroll<NL>([&](auto K) {
-    constexpr int k = K;
-    __builtin_amdgcn_sched_barrier(0);
-    const double akk = bc<k>(Lr[k]);
-    spd = spd && (akk > 0.0);
-    const double ik = rsq1(akk);
-    const double ik2 = ik * ik;
-    const double nc = -(Lr[k] * ik2);
-    double ne2[MR];
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      const double e = E[r][k];
-      ne2[r] = -(e * ik2);
-      E[r][k] = e * ik;
-    }
-#pragma unroll
-    for (int r = 0; r < MR; ++r) fmac_bc<k>(ns[r], ya, ne2[r]);
-    unroll<NL - 1 - k>([&](auto J) {
-      constexpr int j = k + 1 + J;
-#pragma unroll
-      for (int r = 0; r < MR; ++r) fmac_bc<k>(E[r][j], Lr[j], ne2[r]);
-      fmac_bc<k>(Lr[j], Lr[j], nc);
+  if constexpr (kMfma) {
+    // ---- H = L L^T and y = L^{-1} f in one right-looking sweep (VALU).
+    // Step k: pr = row k of the Schur complement (lane k's Lr, read by the
+    // DPP-fused FMAs) = column k by symmetry.  y_k = f_k / sqrt(akk) and
+    // 1 / L[k][k] = 1 / sqrt(akk) are broadcast and captured in LDS by
+    // same-address stores (inside L's area, which is written afterwards).
+    double *ycap = Lp + OFF_Y;
+    unroll<NL>([&](auto K) {
+      constexpr int k = K;
+      __builtin_amdgcn_sched_barrier(0);
+      const double akk = bc<k>(Lr[k]);
+      spd = spd && (akk > 0.0);
+      const double ik = rsq1(akk);
+      const double ik2 = ik * ik;
+      const double nc = -(Lr[k] * ik2);
+      *reinterpret_cast<double2 *>(&ycap[2 * k]) = make_double2(bc<k>(ya) * ik, ik);
+      unroll<NL - 1 - k>([&](auto J) {
+        constexpr int j = k + 1 + J;
+        fmac_bc<k>(Lr[j], Lr[j], nc);
+      });
+      fmac_bc<k>(ya, ya, nc);  // lane k's own f_k becomes 0 (dead; y_k is captured)
+      Lr[k] *= ik;
+      pin(Lr[k]);
     });
-    fmac_bc<k>(ya, ya, nc);  // lane k's own f_k becomes 0 (dead)
-    Lr[k] *= ik;
-  });
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int r = 0; r < MR; ++r) s[r] = -ns[r];
-  // L -> LDS, packed rows (lane l writes row l), kept for the final solves.
-  // Lane l also writes its dead entries j > l, over the start of later rows:
-  // stores go in descending j, and a row's own entry at such an address has
-  // a smaller j, so it lands last (a wave's DS instructions execute in order).
-  unroll<NL>([&](auto J) {
-    constexpr int j = NL - 1 - J;
-    Lp[lrow(l) + j] = Lr[j];
+    __builtin_amdgcn_sched_barrier(0);
     wave_lds_sync();
-  });
+    const int lq = l & 3, lb4 = l & ~3;  // position in the 4 x 4 block, block start
+    const double yl = ycap[2 * l];
+    double iv[4];  // 1 / L[i][i] of the block's rows
+#pragma unroll
+    for (int i = 0; i < 4; ++i) iv[i] = ycap[2 * (lb4 + i) + 1];
+    // ---- D = A L^{-T} on the matrix cores.  Lane (k = row of the wave, b =
+    // lane bits 2-3, c = lane & 3) works for QP b, reading the LDS of slot b.
+    const int mk = (threadIdx.x >> 4) & 3, mb = (threadIdx.x >> 2) & 3, mc = threadIdx.x & 3;
+    double *bb = lds + (((mb & 1) << 1) | (mb >> 1)) * SLOT;  // slot of QP b
+    const double *Tb = bb + OFF_T;
+    double Xt[4][4];
+    auto read_xt = [&]() {
+#pragma unroll
+      for (int K = 0; K < 4; ++K)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Xt[K][i] = Tb[(4 * i + mc) * RS + 4 * K + mk];
+    };
+    wave_lds_sync();
+    // L -> LDS, packed rows (lane l writes row l), kept for the final solves
+    // (over the captures, read above).  Lane l also writes its dead entries
+    // j > l, over the start of later rows: stores go in descending j, and a
+    // row's own entry at such an address has a smaller j, so it lands last (a
+    // wave's DS instructions execute in order).
+    unroll<NL>([&](auto J) {
+      constexpr int j = NL - 1 - J;
+      Lp[lrow(l) + j] = Lr[j];
+      wave_lds_sync();
+    });
+    read_xt();
+    {
+      // column lq of inv(L_BB) for lane l's 4 x 4 diagonal block B: forward
+      // substitution over the block's rows, row i's entries read from lane i
+      // of the quad (quad_perm broadcasts; entries past a row's diagonal are
+      // never read)
+      double lrb[3];  // L[l][lb4 + t], t < 3
+#pragma unroll
+      for (int t = 0; t < 3; ++t) lrb[t] = Lp[lrow(l) + lb4 + t];
+      double x[4];
+      unroll<4>([&](auto I) {
+        constexpr int i = I;
+        double acc = (lq == i) ? 1.0 : 0.0;
+        unroll<i>([&](auto T) {
+          constexpr int t = T;
+          acc = __builtin_fma(-dpp_f64<0x55 * i>(lrb[t]), x[t], acc);
+        });
+        x[i] = acc * iv[i];
+      });
+      *reinterpret_cast<double2 *>(&Tv[4 * l]) = make_double2(x[0], x[1]);
+      *reinterpret_cast<double2 *>(&Tv[4 * l + 2]) = make_double2(x[2], x[3]);
+    }
+    wave_lds_sync();
+    double Ln[4][4], Li[4];
+    const double *Lb = bb + OFF_L;
+#pragma unroll
+    for (int K = 0; K < 4; ++K) {
+      Li[K] = Tb[4 * (4 * K + mk) + mc];
+#pragma unroll
+      for (int J = K + 1; J < 4; ++J) Ln[J][K] = -Lb[lrow(4 * J + mc) + 4 * K + mk];
+    }
+    // one half at a time: the first is in Xt, the second still in av[1]
+#pragma unroll
+    for (int h = 0; h < MR; ++h) {
+      if (h > 0) {
+        stage(av[h]);
+        double row[NL];
+        lds_row16(&Tv[l * RS], row);
+        row_norms(h, row);
+        read_xt();
+      }
+      mfma_fwd_subst(Xt, Ln, Li);
+      // back to rows: D_b(16h + 4i + c, 4K + k) -> slot b's T, lane l reads row l
+      wave_lds_sync();
+#pragma unroll
+      for (int K = 0; K < 4; ++K)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bb[OFF_T + (4 * i + mc) * RS + 4 * K + mk] = Xt[K][i];
+      wave_lds_sync();
+      lds_row16(&Tv[l * RS], E[h]);
+    }
+    wave_lds_sync();
+    // s = b + D y (y one entry per lane, read by the FMAs)
+    double u[MR];
+    dpp_ready(yl);
+    bdot_rows<MR>(yl, E, u);
+#pragma unroll
+    for (int r = 0; r < MR; ++r) s[r] = bl[r] + u[r];
+  } else {
+    // ---- H = L L^T, D = A L^{-T}, y = L^{-1} f: one right-looking sweep.
+    // Step k: pr = row k of the current Schur complement (lane k's Lr, DPP
+    // broadcast) = column k by symmetry, so L[j][k] = pr[j] / sqrt(akk) and
+    //   row l:  Lr[j] -= c pr[j] (j > k),  c = Lr[k] / akk;   Lr[k] = L[l][k]
+    //   D rows: E[k] /= sqrt(akk), E[j] -= E[k] pr[j] / akk (j > k)
+    //   y:      lane-parallel, f_l -= c f_k (f_k read from lane k by the FMA)
+    // Lanes l < k keep updating dead entries of their row (the upper triangle,
+    // never read).  The pivot row is read straight from lane k by the FMAs
+    // (v_fmac_f64_dpp); the sched_barrier and the rsq chain keep every write of
+    // Lr[j] and of f (previous step) well over two instructions before these
+    // reads.  Lane k's own Lr[j] is updated last, after the D rows have read it.
+    // s = b + D y accumulates in the same sweep, negated: D[r][k] y_k =
+    // (e ik)(f_k ik) = -ne2 f_k, one DPP-fused FMA per row with f_k from lane k
+    // (y itself is never formed).
+    double ns[MR];  // -s during the sweep
+#pragma unroll
+    for (int r = 0; r < MR; ++r) ns[r] = -bl[r];
+    unroll<NL>([&](auto K) {
+      constexpr int k = K;
+      __builtin_amdgcn_sched_barrier(0);
+      const double akk = bc<k>(Lr[k]);
+      spd = spd && (akk > 0.0);
+      const double ik = rsq1(akk);
+      const double ik2 = ik * ik;
+      const double nc = -(Lr[k] * ik2);
+      double ne2[MR];
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        const double e = E[r][k];
+        ne2[r] = -(e * ik2);
+        E[r][k] = e * ik;
+      }
+#pragma unroll
+      for (int r = 0; r < MR; ++r) fmac_bc<k>(ns[r], ya, ne2[r]);
+      unroll<NL - 1 - k>([&](auto J) {
+        constexpr int j = k + 1 + J;
+#pragma unroll
+        for (int r = 0; r < MR; ++r) fmac_bc<k>(E[r][j], Lr[j], ne2[r]);
+        fmac_bc<k>(Lr[j], Lr[j], nc);
+      });
+      fmac_bc<k>(ya, ya, nc);  // lane k's own f_k becomes 0 (dead)
+      Lr[k] *= ik;
+    });
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < MR; ++r) s[r] = -ns[r];
+    // L -> LDS, packed rows (lane l writes row l), kept for the final solves
+    // (dead entries j > l first, as above)
+    unroll<NL>([&](auto J) {
+      constexpr int j = NL - 1 - J;
+      Lp[lrow(l) + j] = Lr[j];
+      wave_lds_sync();
+    });
+  }
   // |D[r,:]|^2 = |a_r L^{-T}|^2: the loop's reflections are orthogonal, so it
-  // never changes (the dependency test's scale)
+  // never changes (the dependency test's scale).  Clamped to FLT_MAX instead
+  // of overflowing to inf (rows with |D_r| > 1.8e19, e.g. |a| = 1e20 over a
+  // unit H): the test |d2|^2 > 1e-24 |D_p|^2 then still rejects a dependent
+  // row (|d2|^2 ~ eps^2 |D_p|^2) up to |D_p| ~ 1e23, where it used to reject
+  // every row and end the QP INFEASIBLE.
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
-    ddr[r] = (float)dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; });
+    ddr[r] = __builtin_fminf((float)dot2<NL>([&](int j) { return E[r][j]; }, [&](int j) { return E[r][j]; }),
+                             3.402823466e38f);
     fn2[r] = ddr[r];
   }
   clk.tick(1);
@@ -360,7 +524,10 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
       for (int r = 0; r < MR; ++r) {
         const bool viol = !act[r] && s[r] < thr[r];
-        const float kf = (float)(-s[r]) * __builtin_amdgcn_rsqf(fn2[r]);  // fn2 >= 0 (clamped where it shrinks)
+        // fn2 in [0, FLT_MAX] (clamped where it shrinks); the 2^-100 floor keeps
+        // a violated row's key above 31 -- never 0, the "none violated" key --
+        // when the ratio underflows (row 0 included)
+        const float kf = __builtin_fmaf((float)(-s[r]), __builtin_amdgcn_rsqf(fn2[r]), 0x1p-100f);
         const uint32_t kr = (__float_as_uint(kf) & ~31u) | (uint32_t)(l + NL * r);
         key = viol && kr > key ? kr : key;
       }

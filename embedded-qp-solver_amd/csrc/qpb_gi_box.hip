@@ -189,9 +189,11 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
       // violated bounds (rows of unit norm) ranked by dual steepest edge,
       // -s / |D[l, q:]| as in qpb_gi.hip (the same choices as the dense path
       // on A = [I; -I]): fp32 keys with the row in the low 5 bits, DPP-fused max
-      const float rf = __builtin_amdgcn_rsqf(fn2);  // fn2 >= 0 (clamped where it shrinks)
-      const uint32_t ku = (__float_as_uint((float)(-su) * rf) & ~31u) | (uint32_t)l;
-      const uint32_t kl = (__float_as_uint((float)(-sl) * rf) & ~31u) | (uint32_t)(l + NL);
+      // (fn2 >= 0, clamped where it shrinks; the 2^-100 floor keeps a violated
+      // bound's key nonzero -- 0 is "none violated" -- when the ratio underflows)
+      const float rf = __builtin_amdgcn_rsqf(fn2);
+      const uint32_t ku = (__float_as_uint(__builtin_fmaf((float)(-su), rf, 0x1p-100f)) & ~31u) | (uint32_t)l;
+      const uint32_t kl = (__float_as_uint(__builtin_fmaf((float)(-sl), rf, 0x1p-100f)) & ~31u) | (uint32_t)(l + NL);
       uint32_t key = (!actu && su < thu) ? ku : 0u;
       key = (!actl && sl < thl && kl > key) ? kl : key;
       key = row_max_u32(key);

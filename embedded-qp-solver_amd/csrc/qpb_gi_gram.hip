@@ -1028,8 +1028,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 }  // namespace gram
 }  // namespace qpb
 
-extern "C" hipError_t qpb_workspace(hipStream_t stream, size_t bytes, void **out);
-
 // scratch: per workgroup (NB - QL) D_W rows beyond the LDS ones + the queue head
 extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
                                          const double *b, double *x, double *lam, uint32_t *active,
@@ -1044,12 +1042,11 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
   if (e != hipSuccess) return e;
   const long long grid = d->batch < cus ? d->batch : cus;
   const size_t rows_bytes = (size_t)grid * qpb::gram::SCRATCH * sizeof(double);
-  void *buf = nullptr;
-  e = qpb_workspace(stream, rows_bytes + 256, &buf);  // cached per stream (qpb_workspace.hip)
-  if (e != hipSuccess) return e;
-  int *queue = reinterpret_cast<int *>(static_cast<char *>(buf) + rows_bytes);
-  e = hipMemsetAsync(queue, 0, sizeof(int), stream);
-  if (e == hipSuccess) {
+  // cached per stream (qpb_workspace.hip); the launch is queued under its lock
+  return qpb_with_workspace(stream, rows_bytes + 256, [&](void *buf) {
+    int *queue = reinterpret_cast<int *>(static_cast<char *>(buf) + rows_bytes);
+    hipError_t err = hipMemsetAsync(queue, 0, sizeof(int), stream);
+    if (err != hipSuccess) return err;
     if (sections)
       hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<true>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
                          f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
@@ -1058,7 +1055,6 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
       hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<false>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
                          f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
                          queue, static_cast<double *>(buf), nullptr);
-    e = hipGetLastError();
-  }
-  return e;
+    return hipGetLastError();
+  });
 }

@@ -333,7 +333,9 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       // dual steepest edge as in qpb_gi.hip: the most violated row by
       // -s / |D[l, q:]| (fp32), the row in the low 6 bits (0 = none violated)
       const bool viol = !act && s < thr;
-      const float kf = (float)(-s) * __builtin_amdgcn_rsqf(fn2);  // fn2 >= 0 (clamped where it shrinks)
+      // (fn2 >= 0, clamped where it shrinks; the 2^-100 floor keeps a violated
+      // row's key nonzero when the ratio underflows or fn2 overflows)
+      const float kf = __builtin_fmaf((float)(-s), __builtin_amdgcn_rsqf(fn2), 0x1p-100f);
       uint32_t kk = viol ? ((__float_as_uint(kf) & ~63u) | (uint32_t)l) : 0u;
       kk = row_max_u32(kk);
       const uint32_t k0 = __builtin_amdgcn_readlane(kk, 0), k1 = __builtin_amdgcn_readlane(kk, 16);

@@ -424,8 +424,6 @@ __global__ __launch_bounds__(NT) void ref_invert_kernel(int n, long long batch, 
 
 }  // namespace qpb
 
-extern "C" hipError_t qpb_workspace(hipStream_t stream, size_t bytes, void **out);
-
 namespace {
 // LDS bytes of one workgroup: [P n^2] [M W V 3 n^2 when n <= 64] + 9 vectors
 // + 8 scalars + 2 reduction slots (doubles), perm + 2 (ints)
@@ -434,17 +432,19 @@ size_t ref_lds_bytes(int n, bool with_p) {
   const size_t mats = (with_p ? nn2 : 0) + (n <= qpb::REF_LDS_MAXN ? 3 * nn2 : 0);
   return sizeof(double) * (mats + 9 * (size_t)n + 10) + sizeof(int) * ((size_t)n + 2);
 }
-// n > 64: one workgroup per CU walks the batch, each with its 3 n^2 slice
-hipError_t ref_big_grid(long long batch, int n, hipStream_t stream, unsigned *grid, double **ws) {
+// n > 64: one workgroup per CU walks the batch, each with its 3 n^2 slice of
+// the cached workspace; `launch` queues the kernel while the cache is locked
+hipError_t ref_big_launch(long long batch, int n, hipStream_t stream,
+                          const std::function<void(unsigned grid, double *ws)> &launch) {
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
-  *grid = (unsigned)(batch < cus ? batch : cus);
-  void *p = nullptr;
-  e = qpb_workspace(stream, (size_t)*grid * 3 * (size_t)n * n * sizeof(double), &p);
-  *ws = static_cast<double *>(p);
-  return e;
+  const unsigned grid = (unsigned)(batch < cus ? batch : cus);
+  return qpb_with_workspace(stream, (size_t)grid * 3 * (size_t)n * n * sizeof(double), [&](void *p) {
+    launch(grid, static_cast<double *>(p));
+    return hipGetLastError();
+  });
 }
 template <class K>
 hipError_t allow_lds(K kern, size_t lds) {
@@ -466,12 +466,12 @@ extern "C" hipError_t qpb_launch_ref_invert(int n, long long batch, const double
     hipLaunchKernelGGL(qpb::ref_invert_kernel<64>, dim3((unsigned)batch), dim3(64), lds, stream, n, batch, P, Pinv,
                        nullptr);
   } else {
-    unsigned grid = 0;
-    double *ws = nullptr;
-    hipError_t e = ref_big_grid(batch, n, stream, &grid, &ws);
-    if (e == hipSuccess) e = allow_lds(&qpb::ref_invert_kernel<128>, lds);
+    hipError_t e = allow_lds(&qpb::ref_invert_kernel<128>, lds);
+    if (e == hipSuccess)
+      e = ref_big_launch(batch, n, stream, [&](unsigned grid, double *ws) {
+        hipLaunchKernelGGL(qpb::ref_invert_kernel<128>, dim3(grid), dim3(128), lds, stream, n, batch, P, Pinv, ws);
+      });
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(qpb::ref_invert_kernel<128>, dim3(grid), dim3(128), lds, stream, n, batch, P, Pinv, ws);
   }
   return hipGetLastError();
 }
@@ -495,13 +495,13 @@ extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, con
     hipLaunchKernelGGL(qpb::ref_kernel<64>, dim3((unsigned)d->batch), dim3(64), lds, stream, d->mode, n,
                        (long long)d->batch, d->iterations, d->box_min, d->box_max, P, q, x0, x, iters, nullptr);
   } else {
-    unsigned grid = 0;
-    double *ws = nullptr;
-    hipError_t e = ref_big_grid(d->batch, n, stream, &grid, &ws);
-    if (e == hipSuccess) e = allow_lds(&qpb::ref_kernel<128>, lds);
+    hipError_t e = allow_lds(&qpb::ref_kernel<128>, lds);
+    if (e == hipSuccess)
+      e = ref_big_launch(d->batch, n, stream, [&](unsigned grid, double *ws) {
+        hipLaunchKernelGGL(qpb::ref_kernel<128>, dim3(grid), dim3(128), lds, stream, d->mode, n, (long long)d->batch,
+                           d->iterations, d->box_min, d->box_max, P, q, x0, x, iters, ws);
+      });
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(qpb::ref_kernel<128>, dim3(grid), dim3(128), lds, stream, d->mode, n, (long long)d->batch,
-                       d->iterations, d->box_min, d->box_max, P, q, x0, x, iters, ws);
   }
   return hipGetLastError();
 }

@@ -7,13 +7,22 @@
 // one stream runs in order, so a buffer handed to consecutive launches on the
 // same stream is never used by two of them at once; different streams get
 // different buffers.  Growing frees the old buffer stream-ordered (after the
-// launches already queued on that stream).  qpb_release_workspaces() returns
-// everything (e.g. before hipDeviceReset).
+// launches already queued on that stream).
+//
+// The buffer is only ever handed to a callback that queues its launches
+// while the cache's lock is held (qpb_with_workspace): two host threads
+// sharing a stream (the null stream, say) cannot have one grow -- free --
+// the buffer between the other's lookup and its launch.  A stream must be
+// released (qpb_release_stream_workspace, or qpb_release_workspaces) before
+// the caller destroys it: the cache frees its buffers stream-ordered on it.
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <map>
 #include <mutex>
 #include <utility>
+
+#include "qpb_common.h"  // qpb_with_workspace's declaration
 
 namespace {
 struct Entry {
@@ -24,8 +33,7 @@ std::mutex g_mu;
 std::map<std::pair<int, hipStream_t>, Entry> g_ws;
 }  // namespace
 
-extern "C" __attribute__((visibility("hidden"))) hipError_t qpb_workspace(hipStream_t stream, size_t bytes,
-                                                                          void **out) {
+hipError_t qpb_with_workspace(hipStream_t stream, size_t bytes, const std::function<hipError_t(void *)> &launch) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -43,8 +51,27 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t qpb_workspace(hipStr
     }
     w.bytes = want;
   }
-  *out = w.p;
-  return hipSuccess;
+  return launch(w.p);  // queued on `stream` before any other thread can touch w
+}
+
+extern "C" int qpb_release_stream_workspace(void *stream) {
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(g_mu);
+  int failed = 0, cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto it = g_ws.begin(); it != g_ws.end();) {
+    if (it->first.second != st) {
+      ++it;
+      continue;
+    }
+    if (it->second.p) {
+      (void)hipSetDevice(it->first.first);
+      if (hipFreeAsync(it->second.p, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) ++failed;
+    }
+    it = g_ws.erase(it);
+  }
+  (void)hipSetDevice(cur);
+  return failed ? -3 : 0;  // QPB_ERR_HIP
 }
 
 extern "C" int qpb_release_workspaces(void) {

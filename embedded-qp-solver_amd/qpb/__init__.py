@@ -227,10 +227,33 @@ def active_mask_to_bool(active, m: int):
     return bits.reshape(a.shape[0], -1)[:, :m]
 
 
-def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), stream=None):
-    """Reference-semantics batched solvers (qp_solvers.c replicas) on CUDA tensors."""
+def _require_f64_cuda(name: str, t, shape: tuple):
+    """A contiguous float64 CUDA tensor of exactly `shape`: the C-ABI reads
+    the pointer as device memory of that layout, so a CPU tensor, another
+    dtype or a strided view must be refused here, not dereferenced there."""
     import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+            and tuple(t.shape) == tuple(shape)):
+        got = (tuple(t.shape), str(t.dtype), str(t.device), t.is_contiguous()) if isinstance(t, torch.Tensor) \
+            else type(t).__name__
+        raise ValueError(f"{name}: expected a contiguous float64 CUDA tensor of shape {tuple(shape)}, got {got}")
+
+
+def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), stream=None):
+    """Reference-semantics batched solvers (qp_solvers.c replicas) on CUDA tensors:
+    P (B, n, n), q (B, n), x0 (B, n) or None (zeros)."""
+    import torch
+    if not (isinstance(q, torch.Tensor) and q.dim() == 2):
+        raise ValueError("qpb.ref_solve: q must be a (B, n) tensor")
     B, n = q.shape
+    _require_f64_cuda("qpb.ref_solve: q", q, (B, n))
+    _require_f64_cuda("qpb.ref_solve: P", P, (B, n, n))
+    if x0 is not None:
+        _require_f64_cuda("qpb.ref_solve: x0", x0, (B, n))
+        if x0.device != q.device or P.device != q.device:
+            raise ValueError("qpb.ref_solve: P, q and x0 must be on one device")
+    elif P.device != q.device:
+        raise ValueError("qpb.ref_solve: P and q must be on one device")
     x = torch.empty((B, n), dtype=torch.float64, device=q.device)
     it = torch.empty((B,), dtype=torch.int32, device=q.device)
     d = RefDesc(n, mode, B, iterations, 0, float(box[0]), float(box[1]))
@@ -253,15 +276,24 @@ def matrix_invert(P, stream=None):
 
 
 def qf_eval(P, q, r: float, x, stream=None):
+    """Batched quadratic_form_eval (qp.c:9-27): 1/2 x'Px + q'x + r per QP;
+    P (B, n, n), q (B, n), x (B, n) float64 CUDA tensors."""
     import torch
+    if not (isinstance(q, torch.Tensor) and q.dim() == 2):
+        raise ValueError("qpb.qf_eval: q must be a (B, n) tensor")
     B, n = q.shape
+    _require_f64_cuda("qpb.qf_eval: q", q, (B, n))
+    _require_f64_cuda("qpb.qf_eval: P", P, (B, n, n))
+    _require_f64_cuda("qpb.qf_eval: x", x, (B, n))
+    if not (P.device == q.device == x.device):
+        raise ValueError("qpb.qf_eval: P, q and x must be on one device")
     out = torch.empty((B,), dtype=torch.float64, device=q.device)
     rc = _lib.qpb_qf_eval(n, B, _ptr(P), _ptr(q), float(r), _ptr(x), _ptr(out), _stream_ptr(stream))
     _check(rc, "qpb_qf_eval")
     return out
 
 
-_lib.qpb_solve_sections.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 11
+_lib.qpb_solve_sections.argtypes = [ctypes.POINTER(Desc)] + [_vp] * 10 + [ctypes.c_int64, _vp]
 _lib.qpb_solve_sections.restype = ctypes.c_int
 SECTION_NAMES = ["load", "cholesky", "substitution", "init", "select", "exchange", "back_solve", "step",
                  "add", "drop", "loop_exit", "output"]
@@ -287,7 +319,7 @@ def solve_sections(H, f, A, b, sections, *, max_iter: int = 0, out: Solution | N
     d = Desc(n, m, B, max_iter, 0, 0.0)
     rows = torch.zeros((SECTION_SLOTS, N_SECTIONS), dtype=torch.int64, device=sections.device)
     rc = _lib.qpb_solve_sections(ctypes.byref(d), _ptr(H), _ptr(f), _ptr(A), _ptr(b), _ptr(out.x), _ptr(out.lam),
-                                 _ptr(out.active), _ptr(out.status), _ptr(out.iters), _ptr(rows),
+                                 _ptr(out.active), _ptr(out.status), _ptr(out.iters), _ptr(rows), rows.numel(),
                                  _stream_ptr(stream))
     _check(rc, "qpb_solve_sections")
     sections[:N_SECTIONS] += rows.sum(0)

@@ -4,7 +4,8 @@ One process per GPU (torchrun).  Every QP is independent, so the batch is
 split into contiguous index ranges, one per rank, and each rank solves its
 range with no communication.  The only collective is the optional final
 result gather over RCCL/xGMI (backend "nccl" = RCCL on ROCm; "gloo" on CPU
-for tests): x, lam, active words and status of every rank to every rank.
+for tests): x, lam, active words and status of every rank to rank 0 (or, on
+request, to every rank).
 """
 from __future__ import annotations
 
@@ -32,20 +33,32 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
-def gather_results(local: dict, total: int):
-    """All-gather per-rank result shards (dict of tensors with a leading batch
-    dimension, contiguous shards in rank order) into full-batch tensors on
-    every rank.  Shards may differ in length by one QP (see shard())."""
+def gather_results(local: dict, total: int, dst: int | None = 0):
+    """Gather per-rank result shards (dict of tensors with a leading batch
+    dimension, contiguous shards in rank order) into full-batch tensors.
+
+    dst = rank r (default 0, SURVEY.md §8e's gather to one GPU): rank r gets
+    the full batch, every other rank None -- (world - 1) shards cross the
+    links once.  dst = None: an all-gather, the full batch on every rank
+    (world x the traffic).  Shards may differ in length by one QP (see
+    shard()); they travel padded to the longest and are trimmed here."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size()
+    rank = dist.get_rank()
+    counts = [shard(total, r, world)[1] for r in range(world)]
+    maxc = max(counts)
     out = {}
     for key, t in local.items():
-        counts = [shard(total, r, world)[1] for r in range(world)]
-        maxc = max(counts)
+        if t.shape[0] != counts[rank]:
+            raise ValueError(f"gather_results: {key} has {t.shape[0]} rows, rank {rank}'s shard is {counts[rank]}")
         pad = torch.zeros((maxc,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad)
-        out[key] = torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
-    return out
+        if dst is None:
+            parts = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(parts, pad)
+        else:
+            parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+            dist.gather(pad, parts, dst=dst)
+        out[key] = torch.cat([p[:c] for p, c in zip(parts, counts)], 0) if parts is not None else None
+    return out if (dst is None or rank == dst) else None

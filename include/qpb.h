@@ -179,13 +179,16 @@ int qpb_qf_eval(int32_t n, int64_t batch, const double *P, const double *q,
  * m <= 64) by a build of the kernel with s_memrealtime stamps (100 MHz); adds
  * each wavefront's ticks per kernel section into row (workgroup index mod 256)
  * of sections[256][20] (zero it first; sum the rows for the totals).
+ * sections_len is the device buffer's length in elements: below
+ * QPB_SECTIONS_LEN the call fails with QPB_ERR_INVALID_ARG (no write).
  * n = 16: load, cholesky, substitution, init, select, exchange, back-solve,
  * step, add, drop, loop-exit, output.  16 < n <= 32: load, sweep, init,
  * select, exchange, back-solve, step, add, drop, loop-exit, x, stores. */
+#define QPB_SECTIONS_LEN (256 * 20)
 int qpb_solve_sections(const qpb_desc *desc, const double *H, const double *f,
 		       const double *A, const double *b, double *x, double *lam,
 		       uint32_t *active, int32_t *status, int32_t *iters,
-		       unsigned long long *sections, void *stream);
+		       unsigned long long *sections, int64_t sections_len, void *stream);
 
 /* ------------------------------------------------------------------------
  * On-device input generators.
@@ -250,8 +253,13 @@ int qpb_set_device(int device);
 int qpb_synchronize(void *stream);
 /* Scratch buffers are cached per (device, stream) and reused across calls
  * (the n <= 128 kernels and the reference replicas at n > 64 need one);
- * this synchronises those streams and frees them all. */
+ * this synchronises those streams and frees them all.  The cache frees a
+ * stream's buffer stream-ordered ON that stream, so release a stream's
+ * buffer (qpb_release_stream_workspace) before destroying the stream.  Calls
+ * from several host threads are safe, sharing a stream included: a buffer is
+ * handed to a launch only while the cache is locked. */
 int qpb_release_workspaces(void);
+int qpb_release_stream_workspace(void *stream);
 const char *qpb_last_error(void);
 const char *qpb_version(void);
 

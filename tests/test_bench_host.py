@@ -76,3 +76,24 @@ def test_committed_pmc_matches_the_built_library(bench):
     t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     c = t["config"]
     assert bench.pmc_traffic(c["n"], c["m"], c["batch_per_gpu"], c["family"], qpb.version()) is not None
+
+
+def test_cpu_run_refuses_to_fork_after_gpu_init(bench, monkeypatch):
+    """bench.cpu_run forks one worker per CPU; after this process has
+    initialised the GPU the workers would inherit the HIP runtime (round 3's
+    config-sweep SIGSEGV), so it must refuse instead of forking."""
+    import sys
+    import types
+    fake = types.SimpleNamespace(cuda=types.SimpleNamespace(is_initialized=lambda: True))
+    monkeypatch.setitem(sys.modules, "torch", fake)
+    with pytest.raises(RuntimeError, match="initialised"):
+        bench.cpu_run("ref_admm_batch", 1, [[0.0]], [0.0], 0.1, 1)
+
+
+def test_cpu_run_before_gpu_init_is_allowed(bench, monkeypatch):
+    import sys
+    import types
+    fake = types.SimpleNamespace(cuda=types.SimpleNamespace(is_initialized=lambda: False))
+    monkeypatch.setitem(sys.modules, "torch", fake)
+    # no reference library under this name: returns None without forking
+    assert bench.cpu_run("ref_admm_batch", 1, [[0.0]], [0.0], 0.1, 1, lib_name="absent.so") is None

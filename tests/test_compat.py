@@ -140,3 +140,29 @@ def test_reference_main_builds_against_compat():
     if not os.path.exists(path):
         pytest.skip("reference build not present (needs /root/reference)")
     assert os.access(path, os.X_OK)
+
+
+@pytest.mark.parametrize("n_dim,ok", [(128, True), (129, False), (0, False), (65535, False)])
+def test_compat_init_rejects_ndim_beyond_the_solvers(n_dim, ok):
+    """kmalloc_init() (qpb_compat_init) refuses an N_DIM the GPU solver
+    replicas cannot take, with the reason, at init -- not by exit() inside the
+    caller's first solve.  A child process: the refusal exits, as the
+    reference exits on its own fatal errors (qp_solvers.c:79-82).  Under
+    tests/test_sanitizers.py this runs against the ASan/UBSan build."""
+    import subprocess
+    import sys
+    code = ("import ctypes, os\n"
+            "L = ctypes.CDLL(os.environ['QPB_LIB_UNDER_TEST'])\n"
+            "L.qpb_compat_init.argtypes = [ctypes.c_uint, ctypes.c_double, ctypes.c_double]\n"
+            f"L.qpb_compat_init({n_dim}, -1e12, 1e12)\n"
+            "L.matrix_alloc.restype = ctypes.c_void_p\n"
+            "print('alloc', bool(L.matrix_alloc(0)))\n")
+    env = dict(os.environ, QPB_LIB_UNDER_TEST=LIB)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    if ok:
+        assert r.returncode == 0, r.stderr
+        assert "alloc True" in r.stdout
+    else:
+        assert r.returncode != 0
+        assert f"N_DIM = {n_dim} is outside 1..128" in r.stderr
+        assert "alloc" not in r.stdout

@@ -42,8 +42,12 @@ def _worker(rank, world, port, total, ret):
         xs.append(r.x), lam.append(r.lam), st.append(r.status)
     local = {"x": torch.tensor(np.array(xs).reshape(count, 4)), "lam": torch.tensor(np.array(lam).reshape(count, 8)),
              "status": torch.tensor(np.array(st, dtype=np.int32))}
-    full = gather_results(local, total)
+    full = gather_results(local, total)  # to rank 0
+    every = gather_results(local, total, dst=None)  # all-gather
     t = max_over_ranks(float(rank + 1))
+    assert (full is None) == (rank != 0)
+    for k, v in every.items():
+        ret[f"every_{rank}_{k}"] = v.numpy()
     if rank == 0:
         ret["x"] = full["x"].numpy()
         ret["lam"] = full["lam"].numpy()
@@ -68,3 +72,6 @@ def test_two_rank_shard_solve_gather(total):
     assert np.array_equal(ret["x"], ref)
     assert (ret["status"] == 0).all()
     assert ret["tmax"] == 2.0
+    for r in range(2):  # the all-gather form gives every rank the same batch
+        assert np.array_equal(ret[f"every_{r}_x"], ref)
+        assert np.array_equal(ret[f"every_{r}_lam"], ret["lam"])

@@ -70,9 +70,12 @@ def test_two_rank_qpb_shards_equal_one_batch(qpb, tmp_path, total):
 
 
 def test_bench_gpus_2_runs_two_ranks(qpb):
+    """The N > 1 path SCALE uses (bench.py relaunching itself under
+    torch.distributed.run), with the result gather to rank 0 (--gather) and
+    the self-describing `distributed` block."""
     env = dict(os.environ, QPB_DIST_BACKEND="gloo")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--global-batch", "8192",
-           "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--gather"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -80,3 +83,8 @@ def test_bench_gpus_2_runs_two_ranks(qpb):
     assert line["config"]["global_batch"] == 8192
     assert line["config"]["batch_per_gpu"] == 4096
     assert line["solver_stats"]["ok_frac"] == 1.0
+    d = line["distributed"]
+    assert d["world_size"] == 2 and d["backend"] == "gloo"
+    assert sorted(x["rank"] for x in d["ranks"]) == [0, 1]
+    assert line["gather_ms"] is not None and line["gather_ms"] >= 0.0
+    assert line["gather"]["checked"] is True
