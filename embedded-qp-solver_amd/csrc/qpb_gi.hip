@@ -75,7 +75,7 @@ constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
 // n == 16: D = A L^{-T} on the fp64 matrix cores (v_mfma_f64_4x4x4_4b_f64) by
 // blocked forward substitution; the VALU sweep factorises H only
 #ifndef QPB_GI_MFMA
-#define QPB_GI_MFMA 1
+#define QPB_GI_MFMA 0
 #endif
 constexpr int OFF_Y = 104;  // (y_k, 1/L_kk) captures of the sweep (inside L's area, written after)
 static_assert(SLOT % 2 == 0 && OFF_T % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
@@ -327,6 +327,7 @@ __device__ __forceinline__ void gi_group(
       pin(Lr[k]);
     });
     __builtin_amdgcn_sched_barrier(0);
+    clk.tick(1);
     wave_lds_sync();
     const int lq = l & 3, lb4 = l & ~3;  // position in the 4 x 4 block, block start
     const double yl = ycap[2 * l];
@@ -408,6 +409,7 @@ __device__ __forceinline__ void gi_group(
       lds_row16(&Tv[l * RS], E[h]);
     }
     wave_lds_sync();
+    clk.tick(2);
     // s = b + D y (y one entry per lane, read by the FMAs)
     double u[MR];
     dpp_ready(yl);
@@ -481,7 +483,7 @@ __device__ __forceinline__ void gi_group(
                              3.402823466e38f);
     fn2[r] = ddr[r];
   }
-  clk.tick(1);
+  clk.tick(kMfma ? 3 : 1);
 
   // ------------------------------------------------------ active-set loop
   // R (upper triangular, active positions; column j = position j, column-major

@@ -18,18 +18,29 @@
 // the LU / inverse and two n x n scratch matrices for the per-column solves
 // (thread t keeps its column's vectors in column t: conflict-free) and the
 // n-vectors in LDS.  64 < n <= 128 (the reference's N_DIM is any compile-time
-// size; SURVEY §6 times refC at n = 128): 128-thread workgroups, P and the
-// vectors in LDS (<= 141 KB), the LU and the two scratch matrices in a global
-// workspace slice per workgroup (cached per stream, qpb_workspace.hip), and a
-// grid of one workgroup per CU walking the batch.  The arithmetic is the same
-// code in the same order either way.
+// size; SURVEY §6 times refC at n = 128): 128-thread workgroups with only the
+// vectors in LDS (~10 KB), P, the LU and the two scratch matrices in a global
+// workspace slice per workgroup (4 n^2 doubles, cached per stream,
+// qpb_workspace.hip), and a grid of up to 8 workgroups per CU walking the
+// batch.  P and the LU are stored there column-major, so the row-per-thread
+// accesses (row products, pivot column, Schur update) are coalesced across the
+// wave; W and V stay row-major (the column-per-thread solves).  The arithmetic
+// is the same code in the same order either way: only addresses change.
 #include "qpb_common.h"
 #include "qpb.h"
 
 namespace qpb {
 
 constexpr int REF_MAXN = 128;
-constexpr int REF_LDS_MAXN = 64;  // n above this: matrices M, W, V in global memory
+constexpr int REF_LDS_MAXN = 64;  // n above this: matrices P, M, W, V in global memory
+constexpr int REF_WG_PER_CU = 8;   // n above REF_LDS_MAXN: workgroups per CU in the persistent grid
+// element (r, c) of an n x n matrix: row-major in LDS (NT = 64), column-major
+// in the global workspace (NT = 128, coalesced row-per-thread accesses)
+template <int NT>
+__device__ __forceinline__ int mat_ix(int r, int c, int n) {
+  if constexpr (NT > 64) return c * n + r;
+  return r * n + c;
+}
 
 struct RefShared {
   double *P, *M, *W, *V;  // n*n each (M: LU then inverse is V)
@@ -43,6 +54,13 @@ struct RefShared {
 __device__ __forceinline__ double row_dot(const double *A, const double *v, int i, int n) {
   double acc = 0.0;
   for (int k = 0; k < n; ++k) acc += A[i * n + k] * v[k];
+  return acc;
+}
+// the same with A in the layout of mat_ix<NT>
+template <int NT>
+__device__ __forceinline__ double row_dot_l(const double *A, const double *v, int i, int n) {
+  double acc = 0.0;
+  for (int k = 0; k < n; ++k) acc += A[mat_ix<NT>(i, k, n)] * v[k];
   return acc;
 }
 
@@ -79,7 +97,7 @@ __device__ void ref_invert(RefShared &S, int n) {
     // workgroup and the lowest thread holding it
     double v = 0.0;
     if (tid >= k && tid < n) {
-      v = S.M[tid * n + k];
+      v = S.M[mat_ix<NT>(tid, k, n)];
       v = v < 0 ? -v : v;
     }
     double piv = v;
@@ -107,20 +125,20 @@ __device__ void ref_invert(RefShared &S, int n) {
       S.perm[k] = tmp;
     }
     if (tid < n) {  // matrix_row_permute :472-485 (thread tid swaps column tid)
-      const double a = S.M[pidx * n + tid], b = S.M[k * n + tid];
-      S.M[pidx * n + tid] = b;
-      S.M[k * n + tid] = a;
+      const double a = S.M[mat_ix<NT>(pidx, tid, n)], b = S.M[mat_ix<NT>(k, tid, n)];
+      S.M[mat_ix<NT>(pidx, tid, n)] = b;
+      S.M[mat_ix<NT>(k, tid, n)] = a;
     }
     __syncthreads();
     if (tid > k && tid < n) {  // :523-533
       const int i = tid;
-      double tmp = S.M[i * n + k];
-      tmp /= S.M[k * n + k];
-      S.M[i * n + k] = tmp;
+      double tmp = S.M[mat_ix<NT>(i, k, n)];
+      tmp /= S.M[mat_ix<NT>(k, k, n)];
+      S.M[mat_ix<NT>(i, k, n)] = tmp;
       for (int j = k + 1; j < n; ++j) {
-        double t = S.M[i * n + j];
-        t -= S.M[i * n + k] * S.M[k * n + j];
-        S.M[i * n + j] = t;
+        double t = S.M[mat_ix<NT>(i, j, n)];
+        t -= S.M[mat_ix<NT>(i, k, n)] * S.M[mat_ix<NT>(k, j, n)];
+        S.M[mat_ix<NT>(i, j, n)] = t;
       }
     }
     __syncthreads();
@@ -132,14 +150,14 @@ __device__ void ref_invert(RefShared &S, int n) {
     const int i = tid;
     for (int nn = 0; nn < n; ++nn) {
       double t = 0.0;
-      for (int k = 0; k + 1 <= nn; ++k) t += S.M[nn * n + k] * S.W[k * n + i];
+      for (int k = 0; k + 1 <= nn; ++k) t += S.M[mat_ix<NT>(nn, k, n)] * S.W[k * n + i];
       const double e = (S.perm[nn] == i) ? 1.0 : 0.0;
       S.W[nn * n + i] = e - t;
     }
     for (int nn = n - 1; nn >= 0; --nn) {
       double t = 0.0;
-      for (int k = nn + 1; k < n; ++k) t += S.M[nn * n + k] * S.V[k * n + i];
-      S.V[nn * n + i] = (S.W[nn * n + i] - t) / S.M[nn * n + nn];
+      for (int k = nn + 1; k < n; ++k) t += S.M[mat_ix<NT>(nn, k, n)] * S.V[k * n + i];
+      S.V[nn * n + i] = (S.W[nn * n + i] - t) / S.M[mat_ix<NT>(nn, nn, n)];
     }
   }
   __syncthreads();
@@ -151,10 +169,11 @@ __device__ void ref_invert(RefShared &S, int n) {
 // reference's order), then thread 0 combines them as the reference does.
 // `extra` (>= 0): thread 2 also computes fx + C2 * (t0 . t1) into scal[extra]
 // (the Armijo right-hand side, independent of f(x)).
+template <int NT>
 __device__ double ref_eval(RefShared &S, const double *q, const double *xv, int n, int slot, int extra = -1,
                            double fx = 0.0) {
   const int tid = threadIdx.x;
-  if (tid < n) S.t2[tid] = row_dot(S.P, xv, tid, n);
+  if (tid < n) S.t2[tid] = row_dot_l<NT>(S.P, xv, tid, n);
   __syncthreads();
   if (tid == 0) S.scal[4] = seq_dot(xv, S.t2, n);
   else if (tid == 1) S.scal[5] = seq_dot(q, xv, n);
@@ -171,21 +190,23 @@ __device__ double ref_eval(RefShared &S, const double *q, const double *xv, int 
 }
 
 // grad f(x) = P x + q into out (quadratic_form_eval_grad, qp.c:29-44)
+template <int NT>
 __device__ void ref_grad(RefShared &S, const double *q, const double *xv, double *out, int n) {
   const int tid = threadIdx.x;
   if (tid < n) {
-    const double px = row_dot(S.P, xv, tid, n);
+    const double px = row_dot_l<NT>(S.P, xv, tid, n);
     out[tid] = px + q[tid];
   }
   __syncthreads();
 }
 
 // line_search + armijo (qp_solvers.c:21-63); d in S.d, x in S.x; returns alpha
+template <int NT>
 __device__ double ref_line_search(RefShared &S, const double *q, int n) {
   const int tid = threadIdx.x;
   const double C1 = 0.9;  // C2 = 1e-4 (qp_solvers.c:9) is applied in ref_eval
-  const double fx = ref_eval(S, q, S.x, n, 1);
-  ref_grad(S, q, S.x, S.t0, n);  // grad_fx
+  const double fx = ref_eval<NT>(S, q, S.x, n, 1);
+  ref_grad<NT>(S, q, S.x, S.t0, n);  // grad_fx
   double alpha = 1.0;            // ALPHA0_* (:11-12)
   // The reference loop has no trial cap (:51); alpha *= 0.9 reaches 0 (and
   // then the Armijo test holds) after ~7000 trials for finite data.  The cap
@@ -198,7 +219,7 @@ __device__ double ref_line_search(RefShared &S, const double *q, int n) {
     __syncthreads();
     if (tid < n) S.g[tid] = (S.x[tid] + S.t1[tid]) + S.t1[tid];  // lhs_arg = xk + d_alpha, xk = x + d_alpha
     __syncthreads();
-    const double lhs = ref_eval(S, q, S.g, n, 2, 3, fx);  // and rhs = fx + C2 (grad . d_alpha) in scal[3]
+    const double lhs = ref_eval<NT>(S, q, S.g, n, 2, 3, fx);  // and rhs = fx + C2 (grad . d_alpha) in scal[3]
     const double rhs = S.scal[3];
     if (lhs <= rhs) break;
     alpha *= C1;
@@ -207,21 +228,23 @@ __device__ double ref_line_search(RefShared &S, const double *q, int n) {
 }
 
 // LDS (and workspace) carving shared by the solver and the invert kernels:
-// n <= 64 everything in `sm`; otherwise P (solver only) and the vectors in
-// `sm`, M / W / V in `wsq` (3 n^2 doubles)
+// n <= 64 everything in `sm` (P for the solver only); otherwise the vectors in
+// `sm`, M / W / V / P in `wsq` (the workgroup's 4 n^2 doubles)
+constexpr int REF_WS_MATS = 4;
 template <int NT>
 __device__ __forceinline__ double *ref_carve(RefShared &S, double *sm, double *wsq, int n, bool with_p) {
   const int nn2 = n * n;
   double *cur = sm;
-  if (with_p) {
-    S.P = cur;
-    cur += nn2;
-  }
   if constexpr (NT > 64) {
     S.M = wsq;
     S.W = wsq + nn2;
     S.V = wsq + 2 * nn2;
+    S.P = with_p ? wsq + 3 * nn2 : nullptr;
   } else {
+    if (with_p) {
+      S.P = cur;
+      cur += nn2;
+    }
     S.M = cur;
     S.W = cur + nn2;
     S.V = cur + 2 * nn2;
@@ -238,7 +261,7 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
   const int tid = threadIdx.x;
   RefShared S;
   const int nn2 = n * n;
-  S.x = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * 3 * nn2 : nullptr, n, true);
+  S.x = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * REF_WS_MATS * nn2 : nullptr, n, true);
   // n-vectors packed at stride n: the LDS per QP sets the occupancy
   // (n = 16: 9.6 KB, 16 workgroups per CU)
   S.g = S.x + n;
@@ -254,7 +277,7 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
   S.perm = reinterpret_cast<int *>(S.red + 2);
   S.redi = S.perm + n;
   const double *Pq = Pg + g * (long long)nn2;
-  for (int e = tid; e < nn2; e += blockDim.x) S.P[e] = Pq[e];
+  for (int e = tid; e < nn2; e += blockDim.x) S.P[mat_ix<NT>(e / n, e % n, n)] = Pq[e];
   if (tid < n) {
     q[tid] = qg[g * n + tid];
     S.x[tid] = (mode != QPB_REF_ADMM) ? x0g[g * n + tid] : 0.0;
@@ -270,7 +293,7 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
       ref_invert<NT>(S, n);
     }
     for (; it < iterations; ++it) {
-      ref_grad(S, q, S.x, S.g, n);
+      ref_grad<NT>(S, q, S.x, S.g, n);
       if (tid == 0) S.scal[0] = seq_norm(S.g, n);
       __syncthreads();
       if (MIN_GRAD > S.scal[0]) break;  // :83 / :125
@@ -280,7 +303,7 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
         S.d[tid] = dv;
       }
       __syncthreads();
-      const double alpha = ref_line_search(S, q, n);
+      const double alpha = ref_line_search<NT>(S, q, n);
       if (tid < n) {
         const double da = alpha * S.d[tid];  // scalar_mult(d, alpha)
         S.x[tid] = S.x[tid] + da;            // matrix_add(x, x, d)
@@ -295,7 +318,7 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
     }
     for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = S.P[e];
     __syncthreads();
-    if (tid < n) S.M[tid * n + tid] = S.M[tid * n + tid] + rho;  // R = P + rho I (:285-291)
+    if (tid < n) S.M[mat_ix<NT>(tid, tid, n)] = S.M[mat_ix<NT>(tid, tid, n)] + rho;  // R = P + rho I (:285-291)
     __syncthreads();
     ref_invert<NT>(S, n);  // R^{-1} in S.V (:292)
     const double sq = __builtin_sqrt((double)n);
@@ -408,12 +431,12 @@ __global__ __launch_bounds__(NT) void ref_invert_kernel(int n, long long batch, 
   for (long long g = blockIdx.x; g < batch; g += gridDim.x) {
     RefShared S;
     S.P = nullptr;
-    S.scal = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * 3 * nn2 : nullptr, n, false);
+    S.scal = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * REF_WS_MATS * nn2 : nullptr, n, false);
     S.red = S.scal + 8;
     S.perm = reinterpret_cast<int *>(S.red + 2);
     S.redi = S.perm + n;
     const double *Pq = Pg + g * (long long)nn2;
-    for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = Pq[e];
+    for (int e = tid; e < nn2; e += blockDim.x) S.M[mat_ix<NT>(e / n, e % n, n)] = Pq[e];
     __syncthreads();
     ref_invert<NT>(S, n);
     double *Vq = Vg + g * (long long)nn2;
@@ -429,19 +452,21 @@ namespace {
 // + 8 scalars + 2 reduction slots (doubles), perm + 2 (ints)
 size_t ref_lds_bytes(int n, bool with_p) {
   const size_t nn2 = (size_t)n * n;
-  const size_t mats = (with_p ? nn2 : 0) + (n <= qpb::REF_LDS_MAXN ? 3 * nn2 : 0);
+  const size_t mats = n <= qpb::REF_LDS_MAXN ? (with_p ? nn2 : 0) + 3 * nn2 : 0;
   return sizeof(double) * (mats + 9 * (size_t)n + 10) + sizeof(int) * ((size_t)n + 2);
 }
-// n > 64: one workgroup per CU walks the batch, each with its 3 n^2 slice of
-// the cached workspace; `launch` queues the kernel while the cache is locked
+// n > 64: up to REF_WG_PER_CU workgroups per CU walk the batch, each with its
+// 4 n^2 slice of the cached workspace; `launch` queues the kernel while the
+// cache is locked
 hipError_t ref_big_launch(long long batch, int n, hipStream_t stream,
                           const std::function<void(unsigned grid, double *ws)> &launch) {
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
-  const unsigned grid = (unsigned)(batch < cus ? batch : cus);
-  return qpb_with_workspace(stream, (size_t)grid * 3 * (size_t)n * n * sizeof(double), [&](void *p) {
+  const long long slots = (long long)cus * qpb::REF_WG_PER_CU;
+  const unsigned grid = (unsigned)(batch < slots ? batch : slots);
+  return qpb_with_workspace(stream, (size_t)grid * qpb::REF_WS_MATS * (size_t)n * n * sizeof(double), [&](void *p) {
     launch(grid, static_cast<double *>(p));
     return hipGetLastError();
   });

@@ -171,3 +171,29 @@ def test_qf_eval(qpb):
     out = qpb.qf_eval(dev(g["P"]), dev(g["q"]), 0.0, dev(g["x_exact"]))
     torch.cuda.synchronize()
     assert np.allclose(out.cpu().numpy(), g["f_exact"], rtol=1e-9)
+
+
+def test_n128_grid_reuse_bitwise_vs_live_reference(qpb):
+    """n > 64 runs the replicas as a persistent grid whose workgroups take
+    QP after QP on the same LDS and workspace slice (qpb_ref.hip).  With more
+    QPs than workgroups every slice is reused -- the path a 64-QP batch never
+    reaches: 2 304 reference-generator QPs (more than the grid,
+    which is at most 8 workgroups per CU), matrix_invert and Newton bitwise
+    against the compiled reference, and the generator replica bit-exact over
+    the whole range."""
+    import refc
+    n = 128
+    if not refc.available(n, "1e12"):
+        pytest.skip("oracle/_ref not built")
+    rc = refc.RefC(n, "1e12")
+    B = 2304
+    P, q, x0 = rc.generate(seed=31337, count=B)
+    Pg, qg, xg = qpb.ref_generate(n, B, 31337)
+    assert np.array_equal(Pg.cpu().numpy(), P) and np.array_equal(qg.cpu().numpy(), q)
+    assert np.array_equal(xg.cpu().numpy(), x0)
+    inv = qpb.matrix_invert(Pg).cpu().numpy()
+    pick = np.r_[0:8, 250:262, B - 8:B]  # the first, around the CU count, the last
+    for i in pick:
+        assert np.array_equal(inv[i], rc.invert(P[i].copy())), i
+    x, _ = _run(qpb, qpb.REF_NEWTON, P, q, x0, 10)
+    assert np.array_equal(x, rc.newton(P, q, x0, 10))

@@ -2,7 +2,7 @@
 """A/B timing of libqpb variants (tools/build_variant.sh) on the same batch,
 rounds interleaved so clock/thermal drift hits every variant alike.
   python tools/ab.py name1 name2 ...   ('head' = lib/libqpb.so; name@flags adds qpb_desc.flags)
-env: B (1048576), FAM (box), ROUNDS (5), REPS (6)"""
+env: B (1048576), FAM (box), ROUNDS (5), REPS (6), MAXIT (0 = the default cap; 1 = setup + one trip)"""
 import ctypes
 import json
 import os
@@ -21,6 +21,7 @@ def main(names):
     B = int(os.environ.get("B", 1 << 20))
     fam = os.environ.get("FAM", "box")
     rounds, reps = int(os.environ.get("ROUNDS", 5)), int(os.environ.get("REPS", 6))
+    maxit = int(os.environ.get("MAXIT", 0))
     H, f, A, b = qpb.generate(16, B, 1, family=fam, shift=1.0, box=10.0, device=dev)
     libs, fl = {}, {}
     for nm in names:
@@ -35,7 +36,7 @@ def main(names):
     sols = {nm: qpb.solve(H, f, A, b) for nm in names}
     def call(nm):
         o = sols[nm]
-        d = qpb.Desc(16, 32, B, 0, fl[nm], 0.0)
+        d = qpb.Desc(16, 32, B, maxit, fl[nm], 0.0)
         rc = libs[nm].qpb_solve(ctypes.byref(d), p(H), p(f), p(A), p(b), p(o.x), p(o.lam), p(o.active), p(o.status),
                                 p(o.iters), ctypes.c_void_p(s.cuda_stream))
         assert rc == 0, rc
@@ -61,7 +62,7 @@ def main(names):
         same = bool(torch.equal(sols[nm].x, sols[ref].x) and torch.equal(sols[nm].active, sols[ref].active))
         out[nm or "head"] = {"median_us": round(t[len(t) // 2], 1), "min_us": round(t[0], 1),
                              "same_as_first": same, "iters_mean": float(sols[nm].iters.double().mean())}
-    print(json.dumps({"B": B, "family": fam, "variants": out}, indent=1))
+    print(json.dumps({"B": B, "family": fam, "max_iter": maxit, "variants": out}, indent=1))
 
 
 if __name__ == "__main__":

@@ -53,6 +53,42 @@ __global__ void cost_k(const double *in, double *out, long long *cyc, int iters)
   if (l == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// Pipe sharing: 8 waves per workgroup (two per SIMD: waves w and w + 4 share
+// one); waves 0-3 run independent 4x4x4 f64 MFMAs, waves 4-7 independent
+// v_fma_f64 chains.  MODE 0: MFMA waves only, 1: FMA waves only, 2: both.
+// Concurrent time ~ max of the two: separate pipes; ~ their sum: shared.
+template <int MODE>
+__global__ __launch_bounds__(512) void share_k(const double *in, double *out, long long *cyc, int iters) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  double x = in[l], y = in[l + 64];
+  double c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
+  const bool mf = w < 4;
+  const bool run = MODE == 2 || (MODE == 0 && mf) || (MODE == 1 && !mf);
+  long long t0 = clock64();
+  if (run) {
+    if (mf) {
+      for (int i = 0; i < iters; ++i) {
+        c0 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, c3, 0, 0, 0);
+      }
+    } else {
+      for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          c0 = __builtin_fma(c0, x, y); c1 = __builtin_fma(c1, x, y); c2 = __builtin_fma(c2, x, y);
+          c3 = __builtin_fma(c3, x, y); c4 = __builtin_fma(c4, x, y); c5 = __builtin_fma(c5, x, y);
+          c6 = __builtin_fma(c6, x, y); c7 = __builtin_fma(c7, x, y);
+        }
+      }
+    }
+  }
+  long long t1 = clock64();
+  out[threadIdx.x] = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
+  if (l == 0) cyc[w] = run ? t1 - t0 : 0;
+}
+
 int main() {
   double ha[64], hb[64], hc[64];
   srand(7);
@@ -110,6 +146,26 @@ int main() {
     hipMemcpy(hcyc, dcyc, 32, hipMemcpyDeviceToHost);
     if (rep == 1)
       for (int m = 0; m < 4; ++m) printf("cost: %-36s %.2f cycles per loop trip\n", mn[m], (double)hcyc[m] / iters);
+  }
+  {
+    long long *dc8, h8[8];
+    double *dout;
+    hipMalloc(&dc8, 64);
+    hipMalloc(&dout, 512 * 8);
+    const int it2 = 2048;
+    const char *nm2[3] = {"MFMA waves alone (4 x 4x4x4 f64 per trip)", "FMA waves alone (16 v_fma_f64 per trip)",
+                          "both, one of each per SIMD"};
+    for (int rep = 0; rep < 2; ++rep)
+      for (int m = 0; m < 3; ++m) {
+        if (m == 0) hipLaunchKernelGGL(share_k<0>, dim3(1), dim3(512), 0, 0, da, dout, dc8, it2);
+        if (m == 1) hipLaunchKernelGGL(share_k<1>, dim3(1), dim3(512), 0, 0, da, dout, dc8, it2);
+        if (m == 2) hipLaunchKernelGGL(share_k<2>, dim3(1), dim3(512), 0, 0, da, dout, dc8, it2);
+        hipDeviceSynchronize();
+        hipMemcpy(h8, dc8, 64, hipMemcpyDeviceToHost);
+        if (rep == 1)
+          printf("share: %-44s MFMA waves %.1f, FMA waves %.1f cycles per trip\n", nm2[m],
+                 (double)(h8[0] + h8[1] + h8[2] + h8[3]) / 4 / it2, (double)(h8[4] + h8[5] + h8[6] + h8[7]) / 4 / it2);
+      }
   }
   return 0;
 }
