@@ -61,21 +61,28 @@ def test_wave_kernel_unconstrained_and_ragged(qpb):
         assert np.array_equal(a[5:18], p)
 
 
-def test_wave_kernel_config5_batch(qpb):
-    """BASELINE config 5 shape (n=32, m=64) at a large batch from the on-device
-    generator: every QP certified, a sample against the oracle."""
-    B = 32768
-    H, f, A, b = qpb.generate(32, B, 20261015, family="dense")
+@pytest.mark.parametrize("family", ["dense", "box"])
+def test_wave_kernel_config5_full_batch(qpb, family):
+    """BASELINE configs[4]'s shape at its full batch (n = 32, m = 64,
+    B = 262 144, fp64 default path) from the on-device generator: the KKT
+    certificate on every QP (evaluated on the device), and 48 QPs spread over
+    the whole batch -- the first, the last and random ones -- against the
+    oracle (x, lambda within 1e-6, active set bit-exact)."""
+    from conftest import kkt_max_residual_device
+    B = 262144
+    H, f, A, b = qpb.generate(32, B, 20261015, family=family)
     sol = qpb.solve(H, f, A, b)
     torch.cuda.synchronize()
     st = sol.status.cpu().numpy()
     assert (st == qpb.OK).all(), np.bincount(st)
-    Hn, fn, An, bn = (t.cpu().numpy() for t in (H, f, A, b))
-    x, lam = sol.x.cpu().numpy(), sol.lam.cpu().numpy()
-    r = O.kkt_residuals(Hn, fn, An, bn, x, lam)
-    assert max(float(v.max()) for v in r.values()) <= 1e-9
+    assert kkt_max_residual_device(H, f, A, b, sol.x, sol.lam) <= 1e-9
     mask = qpb.active_mask_to_bool(sol.active.cpu().numpy(), 64)
-    for i in np.random.default_rng(1).choice(B, 12, replace=False):
-        ref = O.active_set_solve(Hn[i], fn[i], An[i], bn[i])
-        assert _relerr(x[i:i + 1], ref.x[None]).max() <= X_TOL
-        assert np.array_equal(mask[i], ref.active)
+    pick = np.r_[0, 1, B - 2, B - 1, np.random.default_rng(5).choice(B, 44, replace=False)]
+    x, lam = sol.x[pick].cpu().numpy(), sol.lam[pick].cpu().numpy()
+    Hn, fn, An, bn = (t[pick].cpu().numpy() for t in (H, f, A, b))
+    for k, i in enumerate(pick):
+        ref = O.active_set_solve(Hn[k], fn[k], An[k], bn[k])
+        assert ref.status == 0
+        assert _relerr(x[k:k + 1], ref.x[None]).max() <= X_TOL, i
+        assert np.array_equal(mask[i], ref.active), i
+        assert np.abs(lam[k] - ref.lam).max() / (1 + np.abs(ref.lam).max()) <= X_TOL, i

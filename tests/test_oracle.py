@@ -119,3 +119,21 @@ def test_scalar_prod_known_answer():
         d = np.arange(N, dtype=np.float64)
         c = d.copy()
         assert float(d @ c) == N * (N + 1) * (2 * N + 1) / 6 - N * N
+
+
+def test_device_kkt_helper_matches_oracle_certificate():
+    """tests/conftest.kkt_max_residual_device (the full-batch certificate of
+    the GPU tests, torch on the device) restates oracle.kkt_residuals: on CPU
+    tensors both give the same worst residual, for exact and perturbed
+    answers."""
+    import torch
+    from conftest import kkt_max_residual_device
+    H, f, A, b = O.family_conditioned(77, 6, 8, m=16, box=3.0, kind="dense")
+    sols = [O.active_set_solve(H[i], f[i], A[i], b[i]) for i in range(6)]
+    x = np.array([s.x for s in sols])
+    lam = np.array([s.lam for s in sols])
+    for xx, ll in ((x, lam), (x + 1e-3, lam), (x, lam - 0.1)):
+        ref = max(float(v.max()) for v in O.kkt_residuals(H, f, A, b, xx, ll).values())
+        t = [torch.from_numpy(np.ascontiguousarray(v)) for v in (H, f, A, b, xx, ll)]
+        got = kkt_max_residual_device(*t, chunk=4)
+        assert abs(got - ref) <= 1e-12 * max(1.0, ref), (got, ref)

@@ -6,7 +6,8 @@
 # usage: VARS="head orig" N=16 M=32 B=1048576 FAM=box PMC_FILE=tools/pmc_ab.txt tools/gpu_pmc_ab.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/pmcab
+OUT=${PMC_OUT:-gpurun_out/pmcab}
+export PMC_OUT=$OUT
 mkdir -p $OUT
 export N=${N:-16} M=${M:-32} B=${B:-1048576} FAM=${FAM:-box} REPS=${REPS:-2}
 for v in ${VARS:-head}; do
@@ -21,8 +22,9 @@ for v in ${VARS:-head}; do
 done
 python3 - <<'PY'
 import csv, collections, glob, json, os, re
+OUT = os.environ["PMC_OUT"]
 out = {}
-for d in sorted(glob.glob("gpurun_out/pmcab/*_*/")):
+for d in sorted(glob.glob(OUT + "/*_*/")):
     v = re.match(r".*/(.+)_\d+/$", d).group(1)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         agg = collections.defaultdict(list)
@@ -32,7 +34,7 @@ for d in sorted(glob.glob("gpurun_out/pmcab/*_*/")):
             agg[(r["Kernel_Name"].split("(")[0][-40:], r["Counter_Name"])].append(float(r["Counter_Value"]))
         for (k, c), vals in agg.items():
             out.setdefault(v, {}).setdefault(k, {})[c] = sum(vals) / len(vals)
-json.dump(out, open("gpurun_out/pmcab/summary.json", "w"), indent=1)
+json.dump(out, open(OUT + "/summary.json", "w"), indent=1)
 for v, ks in out.items():
     for k, cs in ks.items():
         w = cs.get("SQ_WAVES", 1) or 1
