@@ -72,12 +72,6 @@ constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: exchange rows (MR x 16), s_p, 
                                           // cos / sin (16 + 16); y / x capture; lambda scatter
 constexpr int SLOT = OFF_XCH + 34;        // 426 (4 x 426 x 8 B = 13,632 B per wave: 12 waves per CU)
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
-// n == 16: D = A L^{-T} on the fp64 matrix cores (v_mfma_f64_4x4x4_4b_f64) by
-// blocked forward substitution; the VALU sweep factorises H only
-#ifndef QPB_GI_MFMA
-#define QPB_GI_MFMA 0
-#endif
-constexpr int OFF_Y = 104;  // (y_k, 1/L_kk) captures of the sweep (inside L's area, written after)
 static_assert(SLOT % 2 == 0 && OFF_T % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
 static_assert(4 * SLOT * 8 <= 160 * 1024 / 12, "12 waves (3 per SIMD) per CU by LDS");
 static_assert(NL * RS <= SLOT - OFF_T, "input transposes are staged in T + xch");
@@ -119,33 +113,6 @@ __device__ __forceinline__ void bdot_rows(double vec, const double (&x)[MR][NL],
   });
 #pragma unroll
   for (int r = 0; r < MR; ++r) out[r] = a[r][0] + a[r][1];
-}
-
-// v_mfma_f64_4x4x4_4b_f64 (tools/probe/mfma44_probe.hip): block b = lane bits
-// 2-3; A(i,k) at lane i + 4b + 16k, B(k,j) at j + 4b + 16k, C(i,j) at
-// j + 4b + 16i.  Block b carries QP b, whose operands come from slot b's LDS.
-__device__ __forceinline__ double mfma44(double a, double b, double c) {
-  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
-}
-
-// D = A L^{-T} for one 16-row half of A on the matrix cores, as blocked
-// forward substitution in the transposed form (every tile in the C layout of
-// its transpose, so a product feeds the next one with no data movement):
-//   D_K^T = Linv_K X_K^T,   X_J^T -= L_JK D_K^T  (J > K)
-// Xt[K][i]: lane (row k, block b, c) holds X_b(4i + c, 4K + k) of the half;
-// Ln[J][K]: lane (k, b, i) holds -L_b(4J + i, 4K + k) (A layout);
-// Li[K]: lane (k, b, i) holds inv(L_b[KK])(i, k).  On return Xt holds D.
-__device__ __forceinline__ void mfma_fwd_subst(double (&Xt)[4][4], const double (&Ln)[4][4], const double (&Li)[4]) {
-  unroll<4>([&](auto KK) {
-    constexpr int K = KK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Xt[K][i] = mfma44(Li[K], Xt[K][i], 0.0);
-    unroll<3 - K>([&](auto JJ) {
-      constexpr int J = K + 1 + JJ;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Xt[J][i] = mfma44(Ln[J][K], Xt[K][i], Xt[J][i]);
-    });
-  });
 }
 
 // MR: rows of D per lane (m <= 16 MR).  N16: n == 16 (coalesced loads).
@@ -208,8 +175,6 @@ __device__ __forceinline__ void gi_group(
   for (int r = 0; r < MR; ++r) bv[r] = bq[(FULL || l + NL * r < m) ? l + NL * r : 0];
   const double fv = fg[gi * n + (l < n ? l : n - 1)];
   const double fl = (N16 || l < n) ? fv : 0.0;
-  constexpr bool kMfma = N16 && QPB_GI_MFMA;
-  [[maybe_unused]] double2 av[MR][8];  // A as loaded (n == 16)
   [[maybe_unused]] const int hr = l >> 3, hc = 2 * (l & 7);
   // stage 16 rows of a 16-column matrix (as loaded) in this QP's T region
   auto stage = [&](const double2 (&v)[8]) {
@@ -250,6 +215,7 @@ __device__ __forceinline__ void gi_group(
     // all input rows in flight at once (one HBM round trip); instruction
     // selection sinks loads to their first use, so an empty asm consumes
     // them right here
+    double2 av[MR][8];
 #pragma unroll
     for (int r = 0; r < MR; ++r) load_a(r, av[r]);
 #pragma unroll
@@ -263,19 +229,11 @@ __device__ __forceinline__ void gi_group(
     }
     stage(hv);
     lds_row16(&Tv[l * RS], Lr);
-    if constexpr (kMfma) {
-      // the first half of A waits in LDS through the sweep (its row norms now)
-      stage(av[0]);
-      double row[NL];
-      lds_row16(&Tv[l * RS], row);
-      row_norms(0, row);
-    } else {
 #pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        stage(av[r]);
-        lds_row16(&Tv[l * RS], E[r]);
-        row_norms(r, E[r]);
-      }
+    for (int r = 0; r < MR; ++r) {
+      stage(av[r]);
+      lds_row16(&Tv[l * RS], E[r]);
+      row_norms(r, E[r]);
     }
     wave_lds_sync();
   } else {  // padded n < 16: clamped per-lane row loads, identity outside n
@@ -302,121 +260,7 @@ __device__ __forceinline__ void gi_group(
 
   bool spd = true;
   double ya = fl;
-  if constexpr (kMfma) {
-    // ---- H = L L^T and y = L^{-1} f in one right-looking sweep (VALU).
-    // Step k: pr = row k of the Schur complement (lane k's Lr, read by the
-    // DPP-fused FMAs) = column k by symmetry.  y_k = f_k / sqrt(akk) and
-    // 1 / L[k][k] = 1 / sqrt(akk) are broadcast and captured in LDS by
-    // same-address stores (inside L's area, which is written afterwards).
-    double *ycap = Lp + OFF_Y;
-    unroll<NL>([&](auto K) {
-      constexpr int k = K;
-      __builtin_amdgcn_sched_barrier(0);
-      const double akk = bc<k>(Lr[k]);
-      spd = spd && (akk > 0.0);
-      const double ik = rsq1(akk);
-      const double ik2 = ik * ik;
-      const double nc = -(Lr[k] * ik2);
-      *reinterpret_cast<double2 *>(&ycap[2 * k]) = make_double2(bc<k>(ya) * ik, ik);
-      unroll<NL - 1 - k>([&](auto J) {
-        constexpr int j = k + 1 + J;
-        fmac_bc<k>(Lr[j], Lr[j], nc);
-      });
-      fmac_bc<k>(ya, ya, nc);  // lane k's own f_k becomes 0 (dead; y_k is captured)
-      Lr[k] *= ik;
-      pin(Lr[k]);
-    });
-    __builtin_amdgcn_sched_barrier(0);
-    clk.tick(1);
-    wave_lds_sync();
-    const int lq = l & 3, lb4 = l & ~3;  // position in the 4 x 4 block, block start
-    const double yl = ycap[2 * l];
-    double iv[4];  // 1 / L[i][i] of the block's rows
-#pragma unroll
-    for (int i = 0; i < 4; ++i) iv[i] = ycap[2 * (lb4 + i) + 1];
-    // ---- D = A L^{-T} on the matrix cores.  Lane (k = row of the wave, b =
-    // lane bits 2-3, c = lane & 3) works for QP b, reading the LDS of slot b.
-    const int mk = (threadIdx.x >> 4) & 3, mb = (threadIdx.x >> 2) & 3, mc = threadIdx.x & 3;
-    double *bb = lds + (((mb & 1) << 1) | (mb >> 1)) * SLOT;  // slot of QP b
-    const double *Tb = bb + OFF_T;
-    double Xt[4][4];
-    auto read_xt = [&]() {
-#pragma unroll
-      for (int K = 0; K < 4; ++K)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Xt[K][i] = Tb[(4 * i + mc) * RS + 4 * K + mk];
-    };
-    wave_lds_sync();
-    // L -> LDS, packed rows (lane l writes row l), kept for the final solves
-    // (over the captures, read above).  Lane l also writes its dead entries
-    // j > l, over the start of later rows: stores go in descending j, and a
-    // row's own entry at such an address has a smaller j, so it lands last (a
-    // wave's DS instructions execute in order).
-    unroll<NL>([&](auto J) {
-      constexpr int j = NL - 1 - J;
-      Lp[lrow(l) + j] = Lr[j];
-      wave_lds_sync();
-    });
-    read_xt();
-    {
-      // column lq of inv(L_BB) for lane l's 4 x 4 diagonal block B: forward
-      // substitution over the block's rows, row i's entries read from lane i
-      // of the quad (quad_perm broadcasts; entries past a row's diagonal are
-      // never read)
-      double lrb[3];  // L[l][lb4 + t], t < 3
-#pragma unroll
-      for (int t = 0; t < 3; ++t) lrb[t] = Lp[lrow(l) + lb4 + t];
-      double x[4];
-      unroll<4>([&](auto I) {
-        constexpr int i = I;
-        double acc = (lq == i) ? 1.0 : 0.0;
-        unroll<i>([&](auto T) {
-          constexpr int t = T;
-          acc = __builtin_fma(-dpp_f64<0x55 * i>(lrb[t]), x[t], acc);
-        });
-        x[i] = acc * iv[i];
-      });
-      *reinterpret_cast<double2 *>(&Tv[4 * l]) = make_double2(x[0], x[1]);
-      *reinterpret_cast<double2 *>(&Tv[4 * l + 2]) = make_double2(x[2], x[3]);
-    }
-    wave_lds_sync();
-    double Ln[4][4], Li[4];
-    const double *Lb = bb + OFF_L;
-#pragma unroll
-    for (int K = 0; K < 4; ++K) {
-      Li[K] = Tb[4 * (4 * K + mk) + mc];
-#pragma unroll
-      for (int J = K + 1; J < 4; ++J) Ln[J][K] = -Lb[lrow(4 * J + mc) + 4 * K + mk];
-    }
-    // one half at a time: the first is in Xt, the second still in av[1]
-#pragma unroll
-    for (int h = 0; h < MR; ++h) {
-      if (h > 0) {
-        stage(av[h]);
-        double row[NL];
-        lds_row16(&Tv[l * RS], row);
-        row_norms(h, row);
-        read_xt();
-      }
-      mfma_fwd_subst(Xt, Ln, Li);
-      // back to rows: D_b(16h + 4i + c, 4K + k) -> slot b's T, lane l reads row l
-      wave_lds_sync();
-#pragma unroll
-      for (int K = 0; K < 4; ++K)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bb[OFF_T + (4 * i + mc) * RS + 4 * K + mk] = Xt[K][i];
-      wave_lds_sync();
-      lds_row16(&Tv[l * RS], E[h]);
-    }
-    wave_lds_sync();
-    clk.tick(2);
-    // s = b + D y (y one entry per lane, read by the FMAs)
-    double u[MR];
-    dpp_ready(yl);
-    bdot_rows<MR>(yl, E, u);
-#pragma unroll
-    for (int r = 0; r < MR; ++r) s[r] = bl[r] + u[r];
-  } else {
+  {
     // ---- H = L L^T, D = A L^{-T}, y = L^{-1} f: one right-looking sweep.
     // Step k: pr = row k of the current Schur complement (lane k's Lr, DPP
     // broadcast) = column k by symmetry, so L[j][k] = pr[j] / sqrt(akk) and
@@ -463,8 +307,10 @@ __device__ __forceinline__ void gi_group(
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < MR; ++r) s[r] = -ns[r];
-    // L -> LDS, packed rows (lane l writes row l), kept for the final solves
-    // (dead entries j > l first, as above)
+    // L -> LDS, packed rows (lane l writes row l), kept for the final solves.
+    // Lane l also writes its dead entries j > l, over the start of later rows:
+    // stores go in descending j, and a row's own entry at such an address has
+    // a smaller j, so it lands last (a wave's DS instructions execute in order).
     unroll<NL>([&](auto J) {
       constexpr int j = NL - 1 - J;
       Lp[lrow(l) + j] = Lr[j];
@@ -483,7 +329,7 @@ __device__ __forceinline__ void gi_group(
                              3.402823466e38f);
     fn2[r] = ddr[r];
   }
-  clk.tick(kMfma ? 3 : 1);
+  clk.tick(1);
 
   // ------------------------------------------------------ active-set loop
   // R (upper triangular, active positions; column j = position j, column-major

@@ -87,12 +87,6 @@ constexpr int R_KEY = 0;    // per-wave selection keys (NWV)
 constexpr int R_T1 = 8;     // per-wave (ratio min, argmin position) pairs (2 NWV)
 constexpr int R_ND2 = 24;   // per-wave partial |w|^2 (NWV)
 constexpr double kDepTol = 1e-24;
-#ifndef GRAM_RCP_PIVOT
-#define GRAM_RCP_PIVOT 0
-#endif
-#ifndef GRAM_PIPE
-#define GRAM_PIPE 0
-#endif
 constexpr long long SCRATCH = LP + (long long)(NB - QL) * NB;  // doubles per workgroup
 
 using d4 = __attribute__((__vector_size__(4 * sizeof(double)))) double;
@@ -244,28 +238,15 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
       // stay ahead of this step's broadcast and rsq chain, well over the two
       // wait states the v_fmac_f64_dpp reads of a[j] need (hipcc does not pad
       // inline asm; tests/test_dpp_hazards.py checks the built objects)
-#if !GRAM_PIPE
       __builtin_amdgcn_sched_barrier(0);
-#endif
       // pivot row k of the Schur complement = column k (symmetry): lane k's
       // entries, broadcast by DPP
       const double akk = bc<k>(a[k]);
       ok = ok && (akk > 0.0);
-#if GRAM_RCP_PIVOT
-      // the elimination multiplier from 1/akk directly: rcp + one Newton step
-      // is two fp64 operations shorter than rsq1 and its square on the
-      // serial pivot chain; 1/sqrt(akk) (the scaling of L and of the inverse
-      // rows) runs beside it
-      const double iakk = rcp1(akk);
-      const double c = a[k] * iakk;
-      const double ik = rsq1(akk);
-      const double ne2 = -(e[k] * iakk);
-#else
       const double ik = rsq1(akk);  // hardware estimate + one Newton step (qpb_common.h)
       const double ik2 = ik * ik;
       const double c = a[k] * ik2;
       const double ne2 = -(e[k] * ik2);
-#endif
       e[k] *= ik;
       const double nc = -c;
       // broadcasts fused into v_fmac_f64_dpp (the pivot row read straight
@@ -273,26 +254,11 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
       // the same j writes it (volatile asm keeps the order); a[j] was last
       // written in the previous step, well over two instructions before (the
       // DPP read hazard)
-#if GRAM_PIPE
-      // software-pipelined steps (no scheduling barrier): a[k + 1] is updated
-      // first, so the next step's broadcast and reciprocal chain can issue
-      // between this step's remaining FMAs.  The first DPP read of a step may
-      // then follow the previous step's last write directly: it gets the two
-      // wait states itself (fmac_bc_nop); every later read of the step is of
-      // an a[j] written by the previous step's earlier FMAs.
-      unroll<15 - k>([&](auto J) {
-        constexpr int j = k + 1 + J;
-        if constexpr (J == 0) fmac_bc_nop<k>(e[j], a[j], ne2);
-        else fmac_bc<k>(e[j], a[j], ne2);
-        fmac_bc<k>(a[j], a[j], nc);
-      });
-#else
       unroll<15 - k>([&](auto J) {
         constexpr int j = k + 1 + J;
         fmac_bc<k>(e[j], a[j], ne2);
         fmac_bc<k>(a[j], a[j], nc);
       });
-#endif
       a[k] *= ik;
     });
     if (l < 16) {

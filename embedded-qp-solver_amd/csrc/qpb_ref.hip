@@ -33,7 +33,10 @@ namespace qpb {
 
 constexpr int REF_MAXN = 128;
 constexpr int REF_LDS_MAXN = 64;  // n above this: matrices P, M, W, V in global memory
-constexpr int REF_WG_PER_CU = 8;   // n above REF_LDS_MAXN: workgroups per CU in the persistent grid
+#ifndef QPB_REF_WG_PER_CU
+#define QPB_REF_WG_PER_CU 8
+#endif
+constexpr int REF_WG_PER_CU = QPB_REF_WG_PER_CU;  // n above REF_LDS_MAXN: workgroups per CU in the persistent grid
 // element (r, c) of an n x n matrix: row-major in LDS (NT = 64), column-major
 // in the global workspace (NT = 128, coalesced row-per-thread accesses)
 template <int NT>
