@@ -406,17 +406,22 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       rm = (l < q) ? ((l & NH) ? rB : rA) : 0.0;
     }
     clk.tick(5);  // back solve
+    const double t2 = (nd2 > kDepTol * dd) ? -sp * rcp(nd2) : kBig;
     double t1 = kBig;
     int k = 0;
     if (q > 0) {
-      // the packed key only picks k; the step is lane k's exact ratio
       const double ratio = um * rcp(rm);
-      const double tk = wave_min((l < q && rm > 0.0) ? pack_key64(ratio, l) : kBig);
-      k = __builtin_amdgcn_readfirstlane(key_index64(tk));
-      const double tx = readlane_d(ratio, k);
-      t1 = tk < kBig ? tx : kBig;
+      const bool cand = l < q && rm > 0.0;
+      // the reduction only when a candidate ratio is below t2 (a partial step);
+      // otherwise the QP adds p and t1 stays kBig (as qpb_gi.hip)
+      if (__ballot(cand && ratio < t2)) {
+        // the packed key only picks k; the step is lane k's exact ratio
+        const double tk = wave_min(cand ? pack_key64(ratio, l) : kBig);
+        k = __builtin_amdgcn_readfirstlane(key_index64(tk));
+        const double tx = readlane_d(ratio, k);
+        t1 = tk < kBig ? tx : kBig;
+      }
     }
-    const double t2 = (nd2 > kDepTol * dd) ? -sp * rcp(nd2) : kBig;
     const double t = t1 < t2 ? t1 : t2;
     if (!(t < kBig)) {
       status = QPB_INFEASIBLE;

@@ -14,70 +14,120 @@
 // (gcc -O2, x86-64, no FMA) rounds every product and every sum, and so do
 // these kernels, in the same order.
 //
-// Layout: thread i owns row i.  n <= 64: one QP per 64-thread workgroup, P,
-// the LU / inverse and two n x n scratch matrices for the per-column solves
-// (thread t keeps its column's vectors in column t: conflict-free) and the
-// n-vectors in LDS.  64 < n <= 128 (the reference's N_DIM is any compile-time
-// size; SURVEY §6 times refC at n = 128): 128-thread workgroups with only the
-// vectors in LDS (~10 KB), P, the LU and the two scratch matrices in a global
-// workspace slice per workgroup (4 n^2 doubles, cached per stream,
-// qpb_workspace.hip), and a grid of up to 8 workgroups per CU walking the
-// batch.  P and the LU are stored there column-major, so the row-per-thread
-// accesses (row products, pivot column, Schur update) are coalesced across the
-// wave; W and V stay row-major (the column-per-thread solves).  The arithmetic
-// is the same code in the same order either way: only addresses change.
+// Layout: thread i owns row i.
+//   n <= 64: one QP per 64-thread workgroup; P, the LU / inverse and two n x n
+//   scratch matrices for the per-column solves (thread t keeps its column's
+//   vectors in column t: conflict-free) and the n-vectors in LDS.
+//   64 < n <= 128 (the reference's N_DIM is any compile-time size; SURVEY §6
+//   times refC at n = 128): 128-thread workgroups walking the batch, as many
+//   per CU as their LDS allows (one at n = 128), each with ONE n x n matrix X
+//   in LDS at column stride ld = n | 1 (odd: walks along a row and along a
+//   column across the threads are both conflict-free).  X holds in turn the
+//   matrix being factorised (the LU in place), the per-column solves' W and
+//   then V (in place: V[nn] overwrites W[nn] once it is read), and P for the
+//   solver's loop.  The LU factors and, for Newton, the inverse (row
+//   products, coalesced) go to a 2 n^2 slice per workgroup in global memory,
+//   which stays in L2; the solves stage LU row nn into an LDS row buffer (one
+//   element per thread, loaded a step ahead), read there by every thread at
+//   the same address.  Every sequential sum and the LU's row update run in
+//   RC-aligned chunks, loads ahead of the arithmetic, with no branch inside a
+//   chunk (X has ref_npad(n) columns so a chunk never leaves it).  Rounds 3-4
+//   kept all four matrices in a global slice with 8 workgroups per CU: one
+//   dependent memory round trip per multiply-add, 128-156 ms for configs[3]'s
+//   Newton replicas (74 ms now).
+// The arithmetic is the same code in the same order in both layouts: only the
+// addresses, and the grouping of loads ahead of the stores, change.
 #include "qpb_common.h"
 #include "qpb.h"
 
 namespace qpb {
 
 constexpr int REF_MAXN = 128;
-constexpr int REF_LDS_MAXN = 64;  // n above this: matrices P, M, W, V in global memory
-#ifndef QPB_REF_WG_PER_CU
-#define QPB_REF_WG_PER_CU 8
-#endif
-constexpr int REF_WG_PER_CU = QPB_REF_WG_PER_CU;  // n above REF_LDS_MAXN: workgroups per CU in the persistent grid
-// element (r, c) of an n x n matrix: row-major in LDS (NT = 64), column-major
-// in the global workspace (NT = 128, coalesced row-per-thread accesses)
-template <int NT>
-__device__ __forceinline__ int mat_ix(int r, int c, int n) {
-  if constexpr (NT > 64) return c * n + r;
-  return r * n + c;
-}
+constexpr int REF_LDS_MAXN = 64;  // n above this: the one-matrix layout (X) below
+constexpr int REF_BIG_NT = 128;
+constexpr int REF_WS_MATS = 2;  // big layout, per workgroup: the LU factors (row-major), V (column-major)
+constexpr int REF_MAX_WG_PER_CU = 8;
+__host__ __device__ constexpr int ref_ld(int n) { return n | 1; }
+// the big layout's X has ref_npad(n) columns (rows of W / V): every RC-chunk
+// of a row or column stays inside it
+__host__ __device__ constexpr int ref_npad(int n) { return (n + 15) & ~15; }
+
+// an n x n matrix in any layout: element (r, c) at p[r * rs + c * cs]
+struct Mat {
+  double *p;
+  int rs, cs;
+  __device__ __forceinline__ double &operator()(int r, int c) const { return p[r * rs + c * cs]; }
+};
 
 struct RefShared {
-  double *P, *M, *W, *V;  // n*n each (M: LU then inverse is V)
+  Mat P, V;            // the solver's P and the inverse (layout depends on the path)
+  double *M, *W, *Vr;  // n <= 64: LU, W, V row-major in LDS
+  double *X, *Mg;      // n > 64: the LDS matrix, the global LU copy
+  double *rowbuf;      // n > 64: two staged LU rows (2 npad); the LU's dummy store slots
+  int ld;
   double *x, *g, *d, *t0, *t1, *t2;  // n each
   double *scal;                       // scalars broadcast by thread 0
   double *red;                        // cross-wave reduction slots (2)
   int *perm, *redi;
 };
 
-// prod_i = sum_k A[i][k] * v[k], k ascending (matrix_mult, matrix_ops.c:262-270)
-__device__ __forceinline__ double row_dot(const double *A, const double *v, int i, int n) {
+// The sequential sums below keep the reference's order (k ascending, one
+// rounding per product and per sum); their operands are loaded RC at a time
+// ahead of the arithmetic (one memory latency per RC terms, not per term).
+constexpr int RC = 16;
+
+// prod_i = sum_k A(i, k) * v[k], k ascending (matrix_mult, matrix_ops.c:262-270)
+__device__ __forceinline__ double row_dot(const Mat &A, const double *v, int i, int n) {
   double acc = 0.0;
-  for (int k = 0; k < n; ++k) acc += A[i * n + k] * v[k];
-  return acc;
-}
-// the same with A in the layout of mat_ix<NT>
-template <int NT>
-__device__ __forceinline__ double row_dot_l(const double *A, const double *v, int i, int n) {
-  double acc = 0.0;
-  for (int k = 0; k < n; ++k) acc += A[mat_ix<NT>(i, k, n)] * v[k];
+  int k = 0;
+  for (; k + RC <= n; k += RC) {
+    double a[RC], b[RC];
+#pragma unroll
+    for (int u = 0; u < RC; ++u) {
+      a[u] = A(i, k + u);
+      b[u] = v[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < RC; ++u) acc += a[u] * b[u];
+  }
+  for (; k < n; ++k) acc += A(i, k) * v[k];
   return acc;
 }
 
 // matrix_scalar_prod (matrix_ops.c:295-297): sequential
 __device__ __forceinline__ double seq_dot(const double *a, const double *b, int n) {
   double acc = 0.0;
-  for (int k = 0; k < n; ++k) acc += a[k] * b[k];
+  int k = 0;
+  for (; k + RC <= n; k += RC) {
+    double x[RC], y[RC];
+#pragma unroll
+    for (int u = 0; u < RC; ++u) {
+      x[u] = a[k + u];
+      y[u] = b[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < RC; ++u) acc += x[u] * y[u];
+  }
+  for (; k < n; ++k) acc += a[k] * b[k];
   return acc;
 }
 
 // matrix_norm (matrix_ops.c:647-655)
 __device__ __forceinline__ double seq_norm(const double *a, int n) {
   double acc = 0.0;
-  for (int k = 0; k < n; ++k) {
+  int k = 0;
+  for (; k + RC <= n; k += RC) {
+    double x[RC];
+#pragma unroll
+    for (int u = 0; u < RC; ++u) x[u] = a[k + u];
+#pragma unroll
+    for (int u = 0; u < RC; ++u) {
+      double t = x[u];
+      t *= t;
+      acc += t;
+    }
+  }
+  for (; k < n; ++k) {
     double t = a[k];
     t *= t;
     acc += t;
@@ -85,85 +135,235 @@ __device__ __forceinline__ double seq_norm(const double *a, int n) {
   return __builtin_sqrt(acc);
 }
 
-// In-place explicit inverse of S.M (n x n), result in S.V (matrix_invert,
-// matrix_ops.c:551-630).  Thread i: row i in the LU, column i in the solves.
-// NT threads (64: one wavefront; 128: two, reduced through LDS).
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// matrix_lup_decompose (matrix_ops.c:487-536) in place on M, the permutation
+// in S.perm.  NT threads (64: one wavefront; 128: two, reduced through LDS);
+// thread i updates row i.
 template <int NT>
-__device__ void ref_invert(RefShared &S, int n) {
+__device__ void ref_lu(RefShared &S, const Mat &M, int n) {
   const int tid = threadIdx.x;
   if (tid < n) S.perm[tid] = tid;
   __syncthreads();
-  bool singular = false;
-  for (int k = 0; k + 1 < n; ++k) {  // matrix_lup_decompose :507
+  for (int k = 0; k + 1 < n; ++k) {  // :507
     // matrix_lup_pivot :449-470: the first row attaining the largest |M[i][k]|
     // (a strict `>` scan from piv = 0), found by an exact max over the
     // workgroup and the lowest thread holding it
     double v = 0.0;
     if (tid >= k && tid < n) {
-      v = S.M[mat_ix<NT>(tid, k, n)];
+      v = M(tid, k);
       v = v < 0 ? -v : v;
     }
-    double piv = v;
+    double piv;
+    int pidx;
+    if constexpr (NT > 64) {
+      // the wave's max (fmin of -v over the DPP rows, then the four rows:
+      // fmin / fmax drop a NaN as the strict `>` scan skips it), its lowest
+      // thread at the max, then the two waves' pairs through LDS with ONE
+      // barrier (wave 0 wins ties: lower rows; a NaN wave max loses)
+      double m = -row_min(-v);
+      m = __builtin_fmax(__builtin_fmax(readlane_d(m, 0), readlane_d(m, 16)),
+                         __builtin_fmax(readlane_d(m, 32), readlane_d(m, 48)));
+      const unsigned long long hit = __ballot(tid >= k && tid < n && v == m);
+      const int w = tid >> 6;
+      if ((tid & 63) == 0) {
+        S.red[w] = m;
+        S.redi[w] = hit ? (tid & ~63) + __builtin_ctzll(hit) : 1 << 30;
+      }
+      __syncthreads();
+      const double m0 = S.red[0], m1 = S.red[1];
+      piv = __builtin_fmax(m0, m1);
+      pidx = (m1 > m0 || m0 != m0) ? S.redi[1] : S.redi[0];
+    } else {
+      piv = v;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) piv = __builtin_fmax(piv, __shfl_xor(piv, off));
-    if constexpr (NT > 64) {
-      if ((tid & 63) == 0) S.red[tid >> 6] = piv;
-      __syncthreads();
-      piv = __builtin_fmax(S.red[0], S.red[1]);
+      for (int off = 32; off >= 1; off >>= 1) piv = __builtin_fmax(piv, __shfl_xor(piv, off));
+      const unsigned long long hit = __ballot(tid >= k && tid < n && v == piv);
+      pidx = __builtin_ctzll(hit);
     }
-    if (!(piv > 0.0)) {  // singular: the reference prints and returns (:511-515)
-      singular = true;
-      break;
-    }
-    const unsigned long long hit = __ballot(tid >= k && tid < n && v == piv);
-    int pidx = __builtin_ctzll(hit);
-    if constexpr (NT > 64) {
-      if ((tid & 63) == 0) S.redi[tid >> 6] = hit ? (tid & ~63) + pidx : 1 << 30;
-      __syncthreads();
-      pidx = S.redi[0] < S.redi[1] ? S.redi[0] : S.redi[1];
-    }
+    if (!(piv > 0.0)) break;  // singular: the reference prints and returns (:511-515)
     if (tid == 0) {  // permutation_swap :434-447
       const int tmp = S.perm[pidx];
       S.perm[pidx] = S.perm[k];
       S.perm[k] = tmp;
     }
     if (tid < n) {  // matrix_row_permute :472-485 (thread tid swaps column tid)
-      const double a = S.M[mat_ix<NT>(pidx, tid, n)], b = S.M[mat_ix<NT>(k, tid, n)];
-      S.M[mat_ix<NT>(pidx, tid, n)] = b;
-      S.M[mat_ix<NT>(k, tid, n)] = a;
+      const double a = M(pidx, tid), b = M(k, tid);
+      M(pidx, tid) = b;
+      M(k, tid) = a;
     }
     __syncthreads();
     if (tid > k && tid < n) {  // :523-533
       const int i = tid;
-      double tmp = S.M[mat_ix<NT>(i, k, n)];
-      tmp /= S.M[mat_ix<NT>(k, k, n)];
-      S.M[mat_ix<NT>(i, k, n)] = tmp;
-      for (int j = k + 1; j < n; ++j) {
-        double t = S.M[mat_ix<NT>(i, j, n)];
-        t -= S.M[mat_ix<NT>(i, k, n)] * S.M[mat_ix<NT>(k, j, n)];
-        S.M[mat_ix<NT>(i, j, n)] = t;
+      double tmp = M(i, k);
+      tmp /= M(k, k);
+      M(i, k) = tmp;
+      // the row's update RC entries at a time: their loads first, then the
+      // arithmetic and the stores (one LDS latency per RC entries)
+      if constexpr (NT > 64) {
+        // the big layout: RC-aligned chunks over the padded columns, no
+        // branch anywhere (a branch per guarded load made every join wait
+        // for all outstanding LDS reads): entries j <= k and j >= n are
+        // computed and stored to this thread's dummy slot
+        const int npad = ref_npad(n);
+        double *dummy = S.rowbuf + tid;
+        for (int j0 = (k + 1) & ~(RC - 1); j0 < npad; j0 += RC) {
+          double a[RC], b[RC];
+#pragma unroll
+          for (int u = 0; u < RC; ++u) {
+            a[u] = M(i, j0 + u);
+            b[u] = M(k, j0 + u);
+          }
+#pragma unroll
+          for (int u = 0; u < RC; ++u) {
+            double t = a[u];
+            t -= tmp * b[u];
+            const int j = j0 + u;
+            *((j > k && j < n) ? &M(i, j) : dummy) = t;
+          }
+        }
+      } else
+      for (int j0 = k + 1; j0 < n; j0 += RC) {
+        double a[RC], b[RC];
+#pragma unroll
+        for (int u = 0; u < RC; ++u)
+          if (j0 + u < n) {
+            a[u] = M(i, j0 + u);
+            b[u] = M(k, j0 + u);
+          }
+#pragma unroll
+        for (int u = 0; u < RC; ++u)
+          if (j0 + u < n) {
+            double t = a[u];
+            t -= tmp * b[u];
+            M(i, j0 + u) = t;
+          }
       }
     }
-    __syncthreads();
+    // NT > 64: the next step's pivot search reads only the thread's own row,
+    // and its barrier comes before anything reads another thread's row
+    if constexpr (NT <= 64) __syncthreads();
   }
-  (void)singular;
+  if constexpr (NT > 64) __syncthreads();
+}
+
+// In-place explicit inverse (matrix_invert, matrix_ops.c:551-630), n <= 64:
+// S.M -> S.Vr.  Thread i: row i in the LU, column i in the solves.
+__device__ void ref_invert_small(RefShared &S, int n) {
+  const Mat M{S.M, n, 1};
+  ref_lu<64>(S, M, n);
   // per-column solves (:594-619): thread i solves for column i; its w/v
   // vectors are column i of W/V, so V ends up as the inverse (:621-625)
+  const int tid = threadIdx.x;
   if (tid < n) {
     const int i = tid;
     for (int nn = 0; nn < n; ++nn) {
       double t = 0.0;
-      for (int k = 0; k + 1 <= nn; ++k) t += S.M[mat_ix<NT>(nn, k, n)] * S.W[k * n + i];
+      for (int k = 0; k + 1 <= nn; ++k) t += M(nn, k) * S.W[k * n + i];
       const double e = (S.perm[nn] == i) ? 1.0 : 0.0;
       S.W[nn * n + i] = e - t;
     }
     for (int nn = n - 1; nn >= 0; --nn) {
       double t = 0.0;
-      for (int k = nn + 1; k < n; ++k) t += S.M[mat_ix<NT>(nn, k, n)] * S.V[k * n + i];
-      S.V[nn * n + i] = (S.W[nn * n + i] - t) / S.M[mat_ix<NT>(nn, nn, n)];
+      for (int k = nn + 1; k < n; ++k) t += M(nn, k) * S.Vr[k * n + i];
+      S.Vr[nn * n + i] = (S.W[nn * n + i] - t) / M(nn, nn);
     }
   }
   __syncthreads();
+  S.V = Mat{S.Vr, n, 1};
+}
+
+// The same for 64 < n <= 128: the matrix in X (column-major, stride ld) on
+// entry; the LU factors go to S.Mg (row-major) and the inverse ends in X
+// row-major (S.V = X with row stride ld).
+__device__ void ref_invert_big(RefShared &S, int n) {
+  const int tid = threadIdx.x;
+  const int ld = S.ld;
+  ref_lu<REF_BIG_NT>(S, Mat{S.X, 1, ld}, n);
+  for (int e = tid; e < n * n; e += REF_BIG_NT) {
+    const int r = e / n, c = e - r * n;
+    S.Mg[e] = S.X[c * ld + r];
+  }
+  __syncthreads();
+  // per-column solves (:594-619), thread i on column i of W, then of V in its
+  // place: entry nn of the column at X[nn * ld + i] (contiguous across the
+  // threads).  Row nn of the LU is staged from the global copy into an LDS
+  // row buffer (double-buffered, one element per thread, loaded a step ahead)
+  // and read there by every thread at the same address.
+  double *rb0 = S.rowbuf, *rb1 = S.rowbuf + ref_npad(n);
+  double *col = S.X + tid;
+  const double *Mg = S.Mg;
+  double pre = tid < n ? Mg[tid] : 0.0;  // row 0
+  for (int nn = 0; nn < n; ++nn) {
+    double *buf = (nn & 1) ? rb1 : rb0;
+    if (tid < n) buf[tid] = pre;
+    if (nn + 1 < n && tid < n) pre = Mg[(nn + 1) * n + tid];
+    __syncthreads();
+    if (tid < n) {
+      // RC terms per step, all loaded ahead; the last, partial chunk adds
+      // its terms k < nn by a select (no branch per term)
+      double t = 0.0;
+      for (int k0 = 0; k0 < nn; k0 += RC) {
+        double mv[RC], wv[RC];
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+          mv[u] = buf[k0 + u];
+          wv[u] = col[(k0 + u) * ld];
+        }
+        if (k0 + RC <= nn) {
+#pragma unroll
+          for (int u = 0; u < RC; ++u) t += mv[u] * wv[u];
+        } else {
+#pragma unroll
+          for (int u = 0; u < RC; ++u) {
+            const double tn = t + mv[u] * wv[u];
+            t = (k0 + u < nn) ? tn : t;
+          }
+        }
+      }
+      const double e = (S.perm[nn] == tid) ? 1.0 : 0.0;
+      col[nn * ld] = e - t;
+    }
+  }
+  pre = tid < n ? Mg[(n - 1) * n + tid] : 0.0;
+  __syncthreads();  // the last forward step's readers are done with its buffer
+  for (int nn = n - 1; nn >= 0; --nn) {
+    double *buf = (nn & 1) ? rb1 : rb0;
+    if (tid < n) buf[tid] = pre;
+    if (nn > 0 && tid < n) pre = Mg[(nn - 1) * n + tid];
+    __syncthreads();
+    if (tid < n) {
+      // terms k = nn + 1 .. n - 1 in RC-aligned chunks; the first and the
+      // last chunk select their terms
+      double t = 0.0;
+      for (int k0 = (nn + 1) & ~(RC - 1); k0 < n; k0 += RC) {
+        double mv[RC], vv[RC];
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+          mv[u] = buf[k0 + u];
+          vv[u] = col[(k0 + u) * ld];
+        }
+        if (k0 > nn && k0 + RC <= n) {
+#pragma unroll
+          for (int u = 0; u < RC; ++u) t += mv[u] * vv[u];
+        } else {
+#pragma unroll
+          for (int u = 0; u < RC; ++u) {
+            const double tn = t + mv[u] * vv[u];
+            t = (k0 + u > nn && k0 + u < n) ? tn : t;
+          }
+        }
+      }
+      col[nn * ld] = (col[nn * ld] - t) / buf[nn];
+    }
+  }
+  __syncthreads();
+  S.V = Mat{S.X, ld, 1};
 }
 
 // f(x) = 1/2 x^T (P x) + q^T x + r (quadratic_form_eval, qp.c:9-27); xv in LDS;
@@ -176,7 +376,7 @@ template <int NT>
 __device__ double ref_eval(RefShared &S, const double *q, const double *xv, int n, int slot, int extra = -1,
                            double fx = 0.0) {
   const int tid = threadIdx.x;
-  if (tid < n) S.t2[tid] = row_dot_l<NT>(S.P, xv, tid, n);
+  if (tid < n) S.t2[tid] = row_dot(S.P, xv, tid, n);
   __syncthreads();
   if (tid == 0) S.scal[4] = seq_dot(xv, S.t2, n);
   else if (tid == 1) S.scal[5] = seq_dot(q, xv, n);
@@ -197,7 +397,7 @@ template <int NT>
 __device__ void ref_grad(RefShared &S, const double *q, const double *xv, double *out, int n) {
   const int tid = threadIdx.x;
   if (tid < n) {
-    const double px = row_dot_l<NT>(S.P, xv, tid, n);
+    const double px = row_dot(S.P, xv, tid, n);
     out[tid] = px + q[tid];
   }
   __syncthreads();
@@ -230,30 +430,67 @@ __device__ double ref_line_search(RefShared &S, const double *q, int n) {
   return alpha;
 }
 
-// LDS (and workspace) carving shared by the solver and the invert kernels:
-// n <= 64 everything in `sm` (P for the solver only); otherwise the vectors in
-// `sm`, M / W / V / P in `wsq` (the workgroup's 4 n^2 doubles)
-constexpr int REF_WS_MATS = 4;
+// LDS (and workspace) carving shared by the solver and the invert kernels.
+// n <= 64: [P n^2 (solver only)] [M W V 3 n^2] in `sm`.  n > 64: [X n ld] in
+// `sm`, the LU copy and V in the workgroup's 2 n^2 slice of `ws`.  The
+// n-vectors, scalars and ints follow.
 template <int NT>
-__device__ __forceinline__ double *ref_carve(RefShared &S, double *sm, double *wsq, int n, bool with_p) {
+__device__ __forceinline__ void ref_carve(RefShared &S, double *sm, double *ws, int n, bool with_p) {
   const int nn2 = n * n;
   double *cur = sm;
   if constexpr (NT > 64) {
-    S.M = wsq;
-    S.W = wsq + nn2;
-    S.V = wsq + 2 * nn2;
-    S.P = with_p ? wsq + 3 * nn2 : nullptr;
+    S.ld = ref_ld(n);
+    S.X = cur;
+    cur += ref_npad(n) * S.ld;
+    S.rowbuf = cur;
+    cur += 2 * ref_npad(n);
+    S.Mg = ws + (size_t)blockIdx.x * REF_WS_MATS * nn2;
+    S.P = Mat{S.X, 1, S.ld};  // where P is loaded (column-major)
   } else {
+    S.ld = n;
     if (with_p) {
-      S.P = cur;
+      S.P = Mat{cur, n, 1};
       cur += nn2;
     }
     S.M = cur;
     S.W = cur + nn2;
-    S.V = cur + 2 * nn2;
+    S.Vr = cur + 2 * nn2;
     cur += 3 * nn2;
   }
-  return cur;
+  // n-vectors packed at stride n: the LDS per QP sets the occupancy
+  // (n = 16: 9.6 KB, 16 workgroups per CU)
+  S.x = cur;
+  S.g = S.x + n;
+  S.d = S.g + n;
+  S.t0 = S.d + n;
+  S.t1 = S.t0 + n;
+  S.t2 = S.t1 + n;
+  S.scal = S.t2 + 4 * n;  // q, u, z sit between t2 and the scalars
+  S.red = S.scal + 8;
+  S.perm = reinterpret_cast<int *>(S.red + 2);
+  S.redi = S.perm + n;
+}
+
+// the matrix the invert starts from: P (+ rho on the diagonal for ADMM),
+// row-major in LDS (n <= 64) or column-major in X
+template <int NT>
+__device__ __forceinline__ void ref_load_m(RefShared &S, const double *Pq, int n, double diag) {
+  const int tid = threadIdx.x;
+  const int nn2 = n * n;
+  if constexpr (NT > 64) {
+    for (int e = tid; e < nn2; e += NT) {
+      const int r = e / n, c = e - r * n;
+      S.X[c * S.ld + r] = Pq[e];
+    }
+  } else {
+    for (int e = tid; e < nn2; e += NT) S.M[e] = S.P.p[e];
+  }
+  __syncthreads();
+  if (diag != 0.0) {  // R = P + rho I (qp_solvers.c:285-291)
+    double *mii = NT > 64 ? &S.X[tid * S.ld + tid] : &S.M[tid * n + tid];
+    if (tid < n) *mii = *mii + diag;
+    __syncthreads();
+  }
 }
 
 // One QP of the reference solvers (thread i owns row i)
@@ -264,23 +501,15 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
   const int tid = threadIdx.x;
   RefShared S;
   const int nn2 = n * n;
-  S.x = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * REF_WS_MATS * nn2 : nullptr, n, true);
-  // n-vectors packed at stride n: the LDS per QP sets the occupancy
-  // (n = 16: 9.6 KB, 16 workgroups per CU)
-  S.g = S.x + n;
-  S.d = S.g + n;
-  S.t0 = S.d + n;
-  S.t1 = S.t0 + n;
-  S.t2 = S.t1 + n;
+  ref_carve<NT>(S, sm, ws, n, true);
   double *q = S.t2 + n;
   double *u = q + n;
   double *z = u + n;
-  S.scal = z + n;
-  S.red = S.scal + 8;
-  S.perm = reinterpret_cast<int *>(S.red + 2);
-  S.redi = S.perm + n;
   const double *Pq = Pg + g * (long long)nn2;
-  for (int e = tid; e < nn2; e += blockDim.x) S.P[mat_ix<NT>(e / n, e % n, n)] = Pq[e];
+  // P row-major in LDS (n <= 64); for n > 64 it is loaded after the invert
+  if constexpr (NT <= 64) {
+    for (int e = tid; e < nn2; e += NT) S.P.p[e] = Pq[e];
+  }
   if (tid < n) {
     q[tid] = qg[g * n + tid];
     S.x[tid] = (mode != QPB_REF_ADMM) ? x0g[g * n + tid] : 0.0;
@@ -291,9 +520,28 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
   if (mode == QPB_REF_NEWTON || mode == QPB_REF_GD) {
     const double MIN_GRAD = 1e-1;  // MIN_GRAD_GRAD / MIN_GRAD_NEWTON (:14-15)
     if (mode == QPB_REF_NEWTON) {  // hessian_inv = invert(copy(P)) (:115-117)
-      for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = S.P[e];
+      ref_load_m<NT>(S, Pq, n, 0.0);
+      if constexpr (NT > 64) {
+        ref_invert_big(S, n);
+        // V to the global slice (column-major: coalesced row products), P into X
+        double *Vg = S.Mg + nn2;
+        for (int e = tid; e < nn2; e += NT) {
+          const int c = e / n, r = e - c * n;
+          Vg[e] = S.X[r * S.ld + c];
+        }
+        __syncthreads();
+        S.V = Mat{Vg, 1, n};
+      } else {
+        ref_invert_small(S, n);
+      }
+    }
+    if constexpr (NT > 64) {
+      for (int e = tid; e < nn2; e += NT) {
+        const int r = e / n, c = e - r * n;
+        S.X[c * S.ld + r] = Pq[e];
+      }
+      S.P = Mat{S.X, 1, S.ld};
       __syncthreads();
-      ref_invert<NT>(S, n);
     }
     for (; it < iterations; ++it) {
       ref_grad<NT>(S, q, S.x, S.g, n);
@@ -319,11 +567,11 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
       z[tid] = 0.0;
       u[tid] = 0.0;
     }
-    for (int e = tid; e < nn2; e += blockDim.x) S.M[e] = S.P[e];
-    __syncthreads();
-    if (tid < n) S.M[mat_ix<NT>(tid, tid, n)] = S.M[mat_ix<NT>(tid, tid, n)] + rho;  // R = P + rho I (:285-291)
-    __syncthreads();
-    ref_invert<NT>(S, n);  // R^{-1} in S.V (:292)
+    ref_load_m<NT>(S, Pq, n, rho);  // R = P + rho I (:285-291)
+    if constexpr (NT > 64)
+      ref_invert_big(S, n);  // R^{-1} in X (:292)
+    else
+      ref_invert_small(S, n);
     const double sq = __builtin_sqrt((double)n);
     // admm_update_x's right-hand side rho (z - u) - q (:146-159) is each
     // thread's own entry, so it is formed at the end of the previous
@@ -385,8 +633,9 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
   if (tid == 0 && itg) itg[g] = it;
 }
 
-// NT = 64: matrices in LDS, one workgroup per QP.  NT = 128: M, W, V in the
-// workgroup's slice of `ws`; the grid walks the batch.
+// NT = 64: one workgroup per QP, everything in LDS.  NT = 128: the big
+// layout (X in LDS, the LU and V in the workgroup's slice of `ws`); the grid
+// walks the batch.
 template <int NT>
 __global__ __launch_bounds__(NT) void ref_kernel(int mode, int n, long long batch, int iterations,
                                                  double box_min, double box_max, const double *__restrict__ Pg,
@@ -433,17 +682,21 @@ __global__ __launch_bounds__(NT) void ref_invert_kernel(int n, long long batch, 
   const int nn2 = n * n;
   for (long long g = blockIdx.x; g < batch; g += gridDim.x) {
     RefShared S;
-    S.P = nullptr;
-    S.scal = ref_carve<NT>(S, sm, NT > 64 ? ws + (size_t)blockIdx.x * REF_WS_MATS * nn2 : nullptr, n, false);
-    S.red = S.scal + 8;
-    S.perm = reinterpret_cast<int *>(S.red + 2);
-    S.redi = S.perm + n;
+    ref_carve<NT>(S, sm, ws, n, false);
     const double *Pq = Pg + g * (long long)nn2;
-    for (int e = tid; e < nn2; e += blockDim.x) S.M[mat_ix<NT>(e / n, e % n, n)] = Pq[e];
-    __syncthreads();
-    ref_invert<NT>(S, n);
+    if constexpr (NT > 64) {
+      ref_load_m<NT>(S, Pq, n, 0.0);
+      ref_invert_big(S, n);
+    } else {
+      for (int e = tid; e < nn2; e += NT) S.M[e] = Pq[e];
+      __syncthreads();
+      ref_invert_small(S, n);
+    }
     double *Vq = Vg + g * (long long)nn2;
-    for (int e = tid; e < nn2; e += blockDim.x) Vq[e] = S.V[e];
+    for (int e = tid; e < nn2; e += NT) {
+      const int r = e / n, c = e - r * n;
+      Vq[e] = S.V(r, c);
+    }
     __syncthreads();
   }
 }
@@ -451,23 +704,27 @@ __global__ __launch_bounds__(NT) void ref_invert_kernel(int n, long long batch, 
 }  // namespace qpb
 
 namespace {
-// LDS bytes of one workgroup: [P n^2] [M W V 3 n^2 when n <= 64] + 9 vectors
-// + 8 scalars + 2 reduction slots (doubles), perm + 2 (ints)
+// LDS bytes of one workgroup: the matrices ([P n^2] [M W V 3 n^2] for
+// n <= 64; X = n ld for n > 64) + 9 vectors + 8 scalars + 2 reduction slots
+// (doubles), perm + 2 (ints)
 size_t ref_lds_bytes(int n, bool with_p) {
   const size_t nn2 = (size_t)n * n;
-  const size_t mats = n <= qpb::REF_LDS_MAXN ? (with_p ? nn2 : 0) + 3 * nn2 : 0;
+  const size_t mats = n <= qpb::REF_LDS_MAXN ? (with_p ? nn2 : 0) + 3 * nn2 : (size_t)qpb::ref_npad(n) * (qpb::ref_ld(n) + 2);
   return sizeof(double) * (mats + 9 * (size_t)n + 10) + sizeof(int) * ((size_t)n + 2);
 }
-// n > 64: up to REF_WG_PER_CU workgroups per CU walk the batch, each with its
-// 4 n^2 slice of the cached workspace; `launch` queues the kernel while the
-// cache is locked
-hipError_t ref_big_launch(long long batch, int n, hipStream_t stream,
+// n > 64: as many workgroups per CU as their LDS allows (one at n = 128, at
+// most REF_MAX_WG_PER_CU) walk the batch, each with its 2 n^2 slice of the
+// cached workspace; `launch` queues the kernel while the cache is locked
+hipError_t ref_big_launch(long long batch, int n, size_t lds, hipStream_t stream,
                           const std::function<void(unsigned grid, double *ws)> &launch) {
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
-  const long long slots = (long long)cus * qpb::REF_WG_PER_CU;
+  long long per_cu = (long long)(160 * 1024 / lds);
+  if (per_cu < 1) per_cu = 1;
+  if (per_cu > qpb::REF_MAX_WG_PER_CU) per_cu = qpb::REF_MAX_WG_PER_CU;
+  const long long slots = (long long)cus * per_cu;
   const unsigned grid = (unsigned)(batch < slots ? batch : slots);
   return qpb_with_workspace(stream, (size_t)grid * qpb::REF_WS_MATS * (size_t)n * n * sizeof(double), [&](void *p) {
     launch(grid, static_cast<double *>(p));
@@ -496,7 +753,7 @@ extern "C" hipError_t qpb_launch_ref_invert(int n, long long batch, const double
   } else {
     hipError_t e = allow_lds(&qpb::ref_invert_kernel<128>, lds);
     if (e == hipSuccess)
-      e = ref_big_launch(batch, n, stream, [&](unsigned grid, double *ws) {
+      e = ref_big_launch(batch, n, lds, stream, [&](unsigned grid, double *ws) {
         hipLaunchKernelGGL(qpb::ref_invert_kernel<128>, dim3(grid), dim3(128), lds, stream, n, batch, P, Pinv, ws);
       });
     if (e != hipSuccess) return e;
@@ -525,7 +782,7 @@ extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, con
   } else {
     hipError_t e = allow_lds(&qpb::ref_kernel<128>, lds);
     if (e == hipSuccess)
-      e = ref_big_launch(d->batch, n, stream, [&](unsigned grid, double *ws) {
+      e = ref_big_launch(d->batch, n, lds, stream, [&](unsigned grid, double *ws) {
         hipLaunchKernelGGL(qpb::ref_kernel<128>, dim3(grid), dim3(128), lds, stream, d->mode, n, (long long)d->batch,
                            d->iterations, d->box_min, d->box_max, P, q, x0, x, iters, ws);
       });

@@ -120,15 +120,16 @@ def test_matrix_invert_rejects_large_n(qpb):
 REF_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref")
 
 
-@pytest.mark.parametrize("n", [4, 16, 32, 48, 128])
+@pytest.mark.parametrize("n", [4, 16, 32, 48, 80, 127, 128])
 def test_replicas_bitwise_vs_live_reference(qpb, n):
-    """Fresh QPs from the reference generator per n (256; 64 at n = 128, where
-    refC's ADMM takes ~60 ms per QP), solved by the compiled reference
-    (oracle/_ref, linked -Bsymbolic so its internal calls stay inside the
-    reference) and by the GPU replicas: matrix_invert, Newton (10 iterations)
-    and ADMM (1e4, default and active box) bitwise equal.  n = 48 is the
-    reference's own default (config.h:5); n > 64 runs the replicas' global-
-    workspace form (qpb_ref.hip)."""
+    """Fresh QPs from the reference generator per n (256; 64 above n = 64,
+    where refC's ADMM takes up to ~60 ms per QP), solved by the compiled
+    reference (oracle/_ref, linked -Bsymbolic so its internal calls stay inside
+    the reference) and by the GPU replicas: matrix_invert, Newton (10
+    iterations) and ADMM (1e4, default and active box) bitwise equal.  n = 48 is
+    the reference's own default (config.h:5); n > 64 runs the replicas' one-
+    matrix LDS form (qpb_ref.hip): n = 80 with three workgroups per CU, n = 127
+    with an odd n (column stride n itself)."""
     import refc
     if not refc.available(n, "1e12") or not refc.available(n, "1e2"):
         pytest.skip("oracle/_ref not built")
@@ -177,10 +178,10 @@ def test_n128_grid_reuse_bitwise_vs_live_reference(qpb):
     """n > 64 runs the replicas as a persistent grid whose workgroups take
     QP after QP on the same LDS and workspace slice (qpb_ref.hip).  With more
     QPs than workgroups every slice is reused -- the path a 64-QP batch never
-    reaches: 2 304 reference-generator QPs (more than the grid,
-    which is at most 8 workgroups per CU), matrix_invert and Newton bitwise
-    against the compiled reference, and the generator replica bit-exact over
-    the whole range."""
+    reaches: 2 304 reference-generator QPs (the grid is one
+    workgroup per CU at n = 128, so each takes about nine), matrix_invert and
+    Newton bitwise against the compiled reference, and the generator replica
+    bit-exact over the whole range."""
     import refc
     n = 128
     if not refc.available(n, "1e12"):

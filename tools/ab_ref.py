@@ -49,7 +49,7 @@ def main(names):
             times[nm].append(a.elapsed_time(e))
     ref = names[0]
     print(json.dumps({"n": n, "B": B, "iterations": iters, "variants": {
-        nm: {"median_ms": sorted(t)[len(t) // 2], "bitwise_as_first": bool(torch.equal(outs[nm][0], outs[ref][0]))}
+        nm: {"median_ms": sorted(t)[len(t) // 2], "bitwise_as_first": bool(torch.equal(outs[nm][0].view(torch.int64), outs[ref][0].view(torch.int64)))}
         for nm, t in times.items()}}, indent=1))
 
 
