@@ -26,11 +26,11 @@ def main():
     dev = torch.device("cuda", 0)
     fam = os.environ.get("FAM", "box")
     out = {}
-    Bmax = 262144
-    H, f, A, b = bench.make_batch(torch, Bmax, 16, fam, 1, dev)
     bs = os.environ.get("BS")
     sizes = [int(x) for x in bs.split(",")] if bs else [4096, 12288, 24576, 36864, 49152, 61440, 65536, 73728,
                                                          98304, 131072, 196608, 262144]
+    Bmax = max(sizes + [262144])
+    H, f, A, b = qpb.generate(16, Bmax, 1, family=fam, shift=1.0, box=10.0, device=dev)
     for B in sizes:
         h, ff, a, bb = H[:B], f[:B], A[:B], b[:B]
         sol = qpb.solve(h, ff, a, bb)
