@@ -151,6 +151,22 @@ def test_replicas_bitwise_vs_live_reference(qpb, n):
     assert np.array_equal(x, ra.admm(P, q, x0, 10000))
 
 
+@pytest.mark.parametrize("n,count,iters", [(80, 8, 20), (128, 8, 20)])
+def test_gd_big_layout_bitwise_vs_live_reference(qpb, n, count, iters):
+    """REF_GD above n = 64 runs on the one-matrix LDS layout with P loaded
+    column-major and no invert (qpb_ref.hip): 20 iterations (~57 Armijo trials
+    each; refC takes ~10 s per QP for 1e4 iterations at n = 128) on fresh
+    reference-generator QPs against the compiled reference."""
+    import refc
+    if not refc.available(n, "1e12"):
+        pytest.skip("oracle/_ref not built")
+    rc = refc.RefC(n, "1e12")
+    P, q, x0 = rc.generate(seed=999 + n, count=count)
+    x, it = _run(qpb, qpb.REF_GD, P, q, x0, iters)
+    assert np.array_equal(x, rc.gd(P, q, x0, iters))
+    assert (it >= 1).all() and (it <= iters).all()
+
+
 @pytest.mark.parametrize("n", [32])
 def test_gd_bitwise_vs_live_reference(qpb, n):
     """REF_GD (qp_solvers.c:65-101, 1e4 iterations, ~57 Armijo trials each)
@@ -198,3 +214,8 @@ def test_n128_grid_reuse_bitwise_vs_live_reference(qpb):
         assert np.array_equal(inv[i], rc.invert(P[i].copy())), i
     x, _ = _run(qpb, qpb.REF_NEWTON, P, q, x0, 10)
     assert np.array_equal(x, rc.newton(P, q, x0, 10))
+    # ADMM (R = P + I inverted, then 1e3 iterations with R^-1 kept in LDS) on
+    # the whole grid, compared on the picked QPs
+    x, _ = _run(qpb, qpb.REF_ADMM, P, q, x0, 1000)
+    for i in pick:
+        assert np.array_equal(x[i], rc.admm(P[i:i + 1], q[i:i + 1], x0[i:i + 1], 1000)[0]), i
