@@ -444,7 +444,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
   double *Lgl = scratch + (long long)blockIdx.x * SCRATCH;
   const Rows QR{lds + OFF_ROWS, Lgl + LP};
   const int T = (n + 15) >> 4, nb = 16 * T;
-  bool first = true;
   for (;;) {
     // lane ids re-derived opaquely per QP: lane-dependent values are not
     // hoisted out of the QP loop (they would stay live across it)
@@ -459,15 +458,14 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       row[t] = 16 * (RT * wv + t) + li;
       rowok[t] = row[t] < m;
     }
-    // the queue is read one QP ahead: the next QP's inputs are pulled into
-    // the caches while this one iterates (see the prefetch below)
-    if (tid == 0) {
-      flags[1] = first ? atomicAdd(queue, 1) : flags[30];
-      flags[30] = atomicAdd(queue, 1);
-    }
-    first = false;
+    // the next QP index from the queue.  (Rounds 2-3 also read the QP after
+    // it and touched one dword per line of its H and A during this QP's
+    // iterations; the six prefetch registers lived across the loop, spilled
+    // there and made the loop wait on the loads: 3.3-3.9 % slower than no
+    // prefetch, profiles/r04/ab/ab128_nopf_*.json.)
+    if (tid == 0) flags[1] = atomicAdd(queue, 1);
     __syncthreads();
-    const long long g = flags[1], gnext = flags[30];
+    const long long g = flags[1];
     if (g >= batch) break;
     const double *Hq = Hg + g * (long long)n * n;
     const double *Aq = Ag + g * (long long)m * n;
@@ -607,23 +605,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     int status = !spd ? QPB_NOT_SPD : (flags[20] ? QPB_INFEASIBLE : QPB_MAX_ITER);
     bool done = status != QPB_MAX_ITER;
     clk.tick(2);
-    // one dword of every 128-byte line of the next QP's H and A: the lines
-    // reach L2 / the Infinity Cache during this QP's iterations (HBM is idle
-    // then); the values are only consumed after the loop
-    constexpr int PF = 6;
-    uint32_t pf[PF];
-    {
-      const long long gn = gnext < batch ? gnext : g;
-      const uint32_t *hn = reinterpret_cast<const uint32_t *>(Hg + gn * (long long)n * n);
-      const uint32_t *an = reinterpret_cast<const uint32_t *>(Ag + gn * (long long)m * n);
-      const int lh = (n * n + 15) >> 4, la = (m * n + 15) >> 4;  // 128-byte lines
-#pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        const int line = tid + NT * u;
-        pf[u] = line < lh ? hn[32 * line] : (line - lh < la ? an[32 * (line - lh)] : 0u);
-      }
-    }
-
     // ------------------------------------------------------- active set
     // G-I's J = L^{-T} [Q1^T Q2] in the form D_W^T = Q1^T R, with R kept as
     // its inverse Z = R^{-1}: the orthonormal rows Q1 (q x n, permuted column
@@ -937,8 +918,6 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       clk.tick(6);
     }
 
-#pragma unroll
-    for (int u = 0; u < PF; ++u) asm volatile("" ::"v"(pf[u]));
     // ------------------------------------------------------------ outputs
     // full multiplier vector by row (vb), the active-set words,
     // g = y + D_W^T lam = y + D^T lam_full: each wave sums its 32 rows of D
