@@ -657,6 +657,12 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     __syncthreads();
     while (!done && it < max_iter) {
       ++it;
+      // lane ids re-derived opaquely per iteration: the addresses built from
+      // them are recomputed in the iteration instead of hoisted out of the
+      // loop, where they lived across it and spilled
+      int tid = threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      const int l = tid & 63, li = l & 15, lk = l >> 4;
       if (selecting) {
         double kmin = red[R_KEY];
 #pragma unroll
