@@ -88,3 +88,45 @@ def test_bench_gpus_2_runs_two_ranks(qpb):
     assert sorted(x["rank"] for x in d["ranks"]) == [0, 1]
     assert line["gather_ms"] is not None and line["gather_ms"] >= 0.0
     assert line["gather"]["checked"] is True
+
+
+def _rccl_worker(rank, port, total, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.path.insert(0, os.path.join(ROOT, "embedded-qp-solver_amd"))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import qpb
+    from qpb.dist import gather_results
+    H, f, A, b = qpb.generate(16, total, 99, family="dense", first=0, device=dev)
+    sol = qpb.solve(H, f, A, b)
+    full = gather_results({k: getattr(sol, k) for k in ("x", "lam", "active", "status")}, total, dst=0)
+    t = torch.tensor([1.5, -2.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.barrier()
+    torch.cuda.synchronize()
+    torch.save({"backend": dist.get_backend(), "reduced": t.cpu(), "device": str(full["x"].device),
+                **{k: v.cpu() for k, v in full.items()}}, os.path.join(out_dir, "rccl.pt"))
+    dist.destroy_process_group()
+
+
+def test_rccl_gather_and_reduce_one_rank(qpb, tmp_path):
+    """The RCCL ("nccl" backend) code path of the multi-GPU line on this box's
+    one GPU: process-group init with device_id, qpb.dist.gather_results
+    (dist.gather of device tensors to rank 0), an all_reduce and a barrier,
+    as bench.py --gpus N --gather runs them per rank.  One rank: the box has
+    one card, and RCCL refuses two ranks on one device (bench.py checks
+    distinct devices).  The gathered batch equals the direct solve."""
+    import torch.multiprocessing as mp
+    total = 4096
+    mp.spawn(_rccl_worker, args=(_port(), total, str(tmp_path)), nprocs=1, join=True)
+    got = torch.load(os.path.join(tmp_path, "rccl.pt"), weights_only=True)
+    assert got["backend"] == "nccl"
+    assert got["device"].startswith("cuda")
+    assert torch.equal(got["reduced"], torch.tensor([1.5, -2.0], dtype=torch.float64))
+    H, f, A, b = qpb.generate(16, total, 99, family="dense", first=0)
+    sol = qpb.solve(H, f, A, b)
+    torch.cuda.synchronize()
+    for k in ("x", "lam", "active", "status"):
+        assert torch.equal(got[k], getattr(sol, k).cpu()), k
