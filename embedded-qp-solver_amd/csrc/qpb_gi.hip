@@ -124,23 +124,19 @@ __device__ __forceinline__ void gi_group(
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
     uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
     long long batch, int max_iter, double feas_tol, int flags, unsigned long long *__restrict__ dbg,
-    long long grp, const int *__restrict__ qlist, int qcount, int *__restrict__ cap_list,
-    int *__restrict__ cap_count, int tid) {
+    long long grp) {
   static_assert(!FULL || N16, "FULL implies n == 16");
   SectionClock<STAMP> clk;
-  const int l = tid & (NL - 1);
-  const int slot = tid >> 4;
-  const int sh = (tid & 63) & ~(NL - 1);  // this row's bit offset in a wave ballot
+  const int l = threadIdx.x & (NL - 1);
+  const int slot = threadIdx.x >> 4;
+  const int sh = (threadIdx.x & 63) & ~(NL - 1);  // this row's bit offset in a wave ballot
   // Rows past the end of the batch (last group only) do not leave: they replay
   // the batch's last QP -- same trip count, so they never extend the wave's
   // loop -- and store nothing.  Every lane of the wave stays live, so the
   // cross-row reads (wave_max4's readlanes) only ever see real QP state.
-  // (second launch of a tail-trimmed solve: the group's QPs come from qlist,
-  // the QPs the first launch did not finish; its last group replays the
-  // list's last QP the same way)
   const long long graw = grp * QPB + slot;
-  const bool live = graw < (qlist ? (long long)qcount : batch);
-  const long long g = qlist ? (long long)qlist[live ? graw : qcount - 1] : (live ? graw : batch - 1);
+  const bool live = graw < batch;
+  const long long g = live ? graw : batch - 1;
   if constexpr (FULL) {
     n = NL;
     m = NL * MR;
@@ -699,42 +695,21 @@ __device__ __forceinline__ void gi_group(
   if (live && l == 0) {
     statg[g] = status;
     if (itg) itg[g] = it;
-    // first launch of a tail-trimmed solve (max_iter = the trip cap): the QP
-    // goes to the second launch's list
-    if (cap_list && status == QPB_MAX_ITER) cap_list[atomicAdd(cap_count, 1)] = (int)g;
   }
   clk.tick(11);
   clk.flush(dbg);
 }
 
-template <int MR, bool N16, bool FULL, bool STAMP = false, int OCC = 2, bool LIST = false>
+template <int MR, bool N16, bool FULL, bool STAMP = false, int OCC = 2>
 __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
     const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
     uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
     long long batch, int max_iter, double feas_tol, int flags = 0,
-    unsigned long long *__restrict__ dbg = nullptr, const int *__restrict__ qlist = nullptr,
-    const int *__restrict__ qcount_p = nullptr, int *__restrict__ cap_list = nullptr,
-    int *__restrict__ cap_count = nullptr) {
+    unsigned long long *__restrict__ dbg = nullptr) {
   __shared__ double lds[QPB * SLOT];
-  if constexpr (!LIST) {
-    // one group per workgroup
-    gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
-                                   flags, dbg, blockIdx.x, nullptr, 0, cap_list, cap_count, threadIdx.x);
-  } else {
-    // second launch of a tail-trimmed solve: a grid-stride walk over the
-    // list's groups on one round of wave slots.  Lane ids re-derived opaquely
-    // per group, so nothing lane-dependent is hoisted out of the walk and kept
-    // live across it (its own instantiation: the walk's loop-carried state
-    // costs a few spills, which the single-group kernel does not pay).
-    const int qcount = *qcount_p;
-    for (long long grp = blockIdx.x; grp * QPB < qcount; grp += gridDim.x) {
-      int tid = threadIdx.x;
-      asm volatile("" : "+v"(tid));
-      gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter,
-                                     feas_tol, flags, dbg, grp, qlist, qcount, nullptr, nullptr, tid);
-    }
-  }
+  gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
+                                 flags, dbg, blockIdx.x);
 }
 
 }  // namespace qpb
@@ -746,53 +721,22 @@ extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const do
   const long long blocks = (d->batch + qpb::QPB - 1) / qpb::QPB;
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
-  auto launch = [&](unsigned grid, int mi, const int *qlist, const int *qcount, int *cap_list, int *cap_count) {
-#define QPB_GI_LAUNCH(MR, N16, FULL)                                                                              \
-  if (qlist)                                                                                                       \
-    hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL, false, 3, true>), dim3(grid), dim3(64), 0, stream, H, \
-                       f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, mi, tol, d->flags, \
-                       nullptr, qlist, qcount, nullptr, nullptr);                                                  \
-  else                                                                                                             \
-    hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL, false, 3>), dim3(grid), dim3(64), 0, stream, H, f, A,  \
-                       b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, mi, tol, d->flags,       \
-                       nullptr, nullptr, nullptr, cap_list, cap_count)
-    const bool n16 = d->n == 16;
-    if (d->m <= 16) {
-      if (n16 && d->m == 16) QPB_GI_LAUNCH(1, true, true);
-      else if (n16) QPB_GI_LAUNCH(1, true, false);
-      else QPB_GI_LAUNCH(1, false, false);
-    } else {
-      if (n16 && d->m == 32) QPB_GI_LAUNCH(2, true, true);  // 3 waves per SIMD (VGPRs and LDS)
-      else if (n16) QPB_GI_LAUNCH(2, true, false);
-      else QPB_GI_LAUNCH(2, false, false);
-    }
+#define QPB_GI_LAUNCH(MR, N16, FULL)                                                                               \
+  hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream, \
+                     H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,    \
+                     d->flags)
+  const bool n16 = d->n == 16;
+  if (d->m <= 16) {
+    if (n16 && d->m == 16) QPB_GI_LAUNCH(1, true, true);
+    else if (n16) QPB_GI_LAUNCH(1, true, false);
+    else QPB_GI_LAUNCH(1, false, false);
+  } else {
+    if (n16 && d->m == 32) QPB_GI_LAUNCH(2, true, true);  // 3 waves per SIMD (VGPRs and LDS)
+    else if (n16) QPB_GI_LAUNCH(2, true, false);
+    else QPB_GI_LAUNCH(2, false, false);
+  }
 #undef QPB_GI_LAUNCH
-    return hipGetLastError();
-  };
-  // Tail trim (qpb.h QPB_FLAG_NO_TAIL_TRIM): a launch's fixed cost is its
-  // iteration tail -- the waves that start last include a few with 2-3x the
-  // mean trip count -- which is 14-25 % of a 65 536-131 072 QP
-  // launch.  First launch: every QP with at most QPB_TAIL_TRIM_TRIPS trips, the
-  // unfinished ones appended to a list; second launch: those QPs from
-  // scratch, a grid-stride walk over the list on one round of wave slots.
-  const bool trim = d->batch <= QPB_TAIL_TRIM_MAX && QPB_TAIL_TRIM_TRIPS < max_iter &&
-                    !(d->flags & (QPB_FLAG_NO_TAIL_TRIM | QPB_FLAG_DIAG_L2 | QPB_FLAG_DIAG_MALL));
-  if (!trim) return launch((unsigned)blocks, max_iter, nullptr, nullptr, nullptr, nullptr);
-  static const int slots = [] {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    return cus * 12;  // resident waves: 3 per SIMD
-  }();
-  const unsigned grid2 = (unsigned)(blocks < slots ? blocks : slots);
-  return qpb_with_workspace(stream, (size_t)(d->batch + 64) * sizeof(int), [&](void *p) {
-    int *count = static_cast<int *>(p), *list = count + 64;
-    hipError_t e = hipMemsetAsync(count, 0, sizeof(int), stream);
-    if (e == hipSuccess) e = launch((unsigned)blocks, QPB_TAIL_TRIM_TRIPS, nullptr, nullptr, list, count);
-    if (e == hipSuccess) e = launch(grid2, max_iter, list, count, nullptr, nullptr);
-    return e;
-  });
+  return hipGetLastError();
 }
 
 // diagnostic: per-section wave ticks of the n=16, 16<m<=32 kernel (sections[256][20])

@@ -102,16 +102,6 @@ typedef enum qpb_error {
 
 /* flag value 128 (the round-1 n <= 128 kernel) is retired: accepted and ignored */
 
-/* n <= 16, m <= 32: batches up to QPB_TAIL_TRIM_MAX QPs are solved in two
- * launches -- every QP with at most QPB_TAIL_TRIM_TRIPS active-set trips, then
- * the QPs that did not finish, re-solved from scratch -- so a launch does not
- * end waiting on the few long QPs of its last waves.  Results are the same as
- * one launch (every QP's arithmetic is independent of its wave-mates).  This
- * flag forces the single launch (A/B measurement). */
-#define QPB_FLAG_NO_TAIL_TRIM 256
-#define QPB_TAIL_TRIM_TRIPS 10
-#define QPB_TAIL_TRIM_MAX (1LL << 30)
-
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */
 	int32_t m;        /* rows of A x <= b, 0..QPB_MAX_M (0: unconstrained) */
