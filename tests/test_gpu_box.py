@@ -132,3 +132,25 @@ def test_box_metric_batch_kkt(qpb):
     Hs, fs, As, bs = (t[idx].cpu().numpy() for t in (H, f, A, b))
     r = O.kkt_residuals(Hs, fs, As, bs, sol.x[idx].cpu().numpy(), sol.lam[idx].cpu().numpy())
     assert max(float(v.max()) for v in r.values()) <= 1e-9
+
+
+@pytest.mark.parametrize("n", [16, 5])
+def test_box_tiny_hessian_only_first_bound_violated(qpb, n):
+    """ADVICE r03 on the box kernel: H = 1e-40 I and f scaled with it, only
+    x_0's upper bound violated at the unconstrained minimiser.  The selection
+    key of that single violated bound must not round to the "none violated"
+    key: x* = (1, -f0[1:]), one active bound."""
+    B = 8
+    rs = np.random.default_rng(n)
+    f0 = rs.uniform(-0.5, 0.5, size=(B, n))
+    f0[:, 0] = -3.0
+    H = np.broadcast_to(np.eye(n), (B, n, n)) * 1e-40
+    lb, ub = -np.ones((B, n)), np.ones((B, n))
+    sol = qpb.solve_box(*_cuda(np.ascontiguousarray(H), f0 * 1e-40, lb, ub))
+    x, lam, act, st, it = _np(sol)
+    assert (st == qpb.OK).all(), st
+    x_ref = -f0.copy()
+    x_ref[:, 0] = 1.0
+    assert np.abs(x - x_ref).max() <= 1e-9
+    mask = qpb.active_mask_to_bool(act, 2 * n)
+    assert mask[:, 0].all() and mask.sum(axis=1).tolist() == [1] * B
