@@ -88,6 +88,9 @@ def test_bench_gpus_2_runs_two_ranks(qpb):
     assert sorted(x["rank"] for x in d["ranks"]) == [0, 1]
     assert line["gather_ms"] is not None and line["gather_ms"] >= 0.0
     assert line["gather"]["checked"] is True
+    # the pipelined leg (two streams per rank, max over ranks) gives the same answers
+    pl = line["pipelined"]
+    assert pl["streams"] == 2 and pl["answers_equal"] is True and pl["value"] > 0.0
 
 
 def _rccl_worker(rank, port, total, out_dir):
