@@ -87,8 +87,8 @@ static int check_device(void) {
 // QPs per launch: a launch's grid holds at most 2^32 - 1 work-items, so each
 // kernel family takes at most 2^32 / (threads per QP) QPs per launch (minus a
 // margin); larger batches are split into consecutive launches on the stream.
-static long long chunk_qps(int n, int m) {
-  if (n <= 16 && m <= 32) return 1LL << 27;  // 16 lanes per QP
+static long long chunk_qps(int n, int m, int flags = 0) {
+  if (n <= 16 && m <= 32 && !(flags & QPB_FLAG_DIAG_WAVE)) return 1LL << 27;  // 16 lanes per QP
   if (n <= 32 && m <= 64) return 1LL << 25;  // 64 lanes per QP
   return 1LL << 21;                          // n <= 128: one workgroup per CU walks the QPs (bounded chunks)
 }
@@ -116,7 +116,7 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
   if (rc) return rc;
   // n <= 16, m <= 32: four QPs per wavefront; n <= 32, m <= 64: one QP per
   // wavefront; larger: one QP per workgroup
-  const long long n = d->n, m = d->m, w = (m + 31) / 32, step = chunk_qps(d->n, d->m);
+  const long long n = d->n, m = d->m, w = (m + 31) / 32, step = chunk_qps(d->n, d->m, d->flags);
   for (long long k0 = 0; k0 < d->batch; k0 += step) {
     qpb_desc c = *d;
     c.batch = d->batch - k0 < step ? d->batch - k0 : step;
@@ -126,7 +126,7 @@ extern "C" int qpb_solve(const qpb_desc *d, const double *H, const double *f, co
     uint32_t *ac = m ? active + k0 * w : active;
     int32_t *sc = status + k0, *ic = iters ? iters + k0 : iters;
     hipError_t e;
-    if (d->n <= 16 && d->m <= 32)
+    if (d->n <= 16 && d->m <= 32 && !(d->flags & QPB_FLAG_DIAG_WAVE))
       e = qpb_launch_gi(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);
     else if (d->n > 16 && d->n <= 32 && d->m <= 64 && (d->flags & QPB_FLAG_MIXED))
       e = qpb_launch_gi_mixed(&c, Hc, fc, Ac, bc, xc, lc, ac, sc, ic, (hipStream_t)stream);

@@ -43,6 +43,7 @@ MAX_N, MAX_M = 128, 256
 # qpb_desc.flags (include/qpb.h)
 FLAG_DIAG_L2, FLAG_DIAG_MALL = 1, 16
 FLAG_MIXED, FLAG_DIAG_NO_REDO = 32, 64
+FLAG_DIAG_WAVE = 256  # n <= 16 solved by the one-QP-per-wavefront kernel (lockstep endpoint; measurement only)
 STATUS_REDO = 100  # internal: a QP the mixed kernel leaves to the fp64 re-solve (FLAG_DIAG_NO_REDO only)
 
 

@@ -101,6 +101,11 @@ typedef enum qpb_error {
 #define QPB_FLAG_DIAG_NO_REDO 64
 
 /* flag value 128 (the round-1 n <= 128 kernel) is retired: accepted and ignored */
+/* diagnostic flag (n <= 16, m <= 32): solve with the one-QP-per-wavefront
+ * kernel of the n <= 32 class (qpb_gi_wave.hip) instead of four QPs per
+ * wavefront -- the group-size-1 endpoint of the lockstep model (DESIGN.md
+ * §2.1); same answers within the parity bars, not a faster path */
+#define QPB_FLAG_DIAG_WAVE 256
 
 typedef struct qpb_desc {
 	int32_t n;        /* variables, 1..QPB_MAX_N */

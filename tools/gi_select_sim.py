@@ -5,7 +5,8 @@ import os, sys, numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'oracle'))
 import oracle
 
-def gi(H, f, A, b, rule, tol=1e-10):
+def gi(H, f, A, b, rule, tol=1e-10, trace=None):
+    # trace: a list that receives (q, 'add' | 'drop') per iteration when given
     n = len(f); m = len(b)
     L = np.linalg.cholesky(H)
     D0 = np.linalg.solve(L, A.T).T          # A L^{-T}
@@ -42,6 +43,8 @@ def gi(H, f, A, b, rule, tol=1e-10):
             if not np.isfinite(t): return it, adds, drops, None
             if np.isfinite(t2): s = s + t * (Dc[:, q:] @ d2)
             lam = lam - t * r; up += t
+            if trace is not None:
+                trace.append((q, 'add' if t2 <= t1 else 'drop'))
             if t2 <= t1:
                 nrm = np.linalg.norm(d2)
                 alpha = -nrm if d2[0] <= 0 else nrm      # kernel: Dpq <= 0 -> -|d2|

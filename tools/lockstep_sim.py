@@ -6,7 +6,8 @@ for (a) the batch order, (b) QPs sorted inside windows of W by their initially
 violated count (a predictor available after the setup) and by the true count
 (the unreachable bound), and (c) a first launch capped at k trips whose
 unfinished QPs are re-solved from scratch in lockstep groups of four (setup
-charged as SETUP trips).  usage: tools/lockstep_sim.py [B] [family]"""
+charged as SETUP trips), and (d) the trips per wave for lockstep groups of
+1, 2, 4 and 8 QPs (tools/group_model.py turns them into issue cycles).  usage: tools/lockstep_sim.py [B] [family]"""
 import os
 import sys
 
@@ -36,6 +37,10 @@ def main(B, fam):
     lock = lambda o: its[o].reshape(-1, 4).max(1).mean()  # noqa: E731
     print(f"{fam}: iterations {its.mean():.3f}, corr(iterations, violated at x0) {np.corrcoef(its, nv)[0, 1]:.2f}")
     print(f"  batch order: {lock(np.arange(B4)):.3f} trips per wave")
+    # group sizes: trips a wavefront of G QPs runs (max over its group), per QP
+    for G in (1, 2, 4, 8):
+        BG = B // G * G
+        print(f"  group size {G}: {its[:BG].reshape(-1, G).max(1).mean() if BG <= B4 else float('nan'):.3f} trips per wave")
     for W in (16, 64):
         for name, key in (("violated count", nv.astype(float)), ("true count", its.astype(float))):
             o = np.concatenate([w0 + np.argsort(key[w0:w0 + W], kind="stable") for w0 in range(0, B4, W)])
