@@ -103,6 +103,29 @@ VALU_COST = {"FMA_F64": 5.24, "MUL_F64": 5.47, "ADD_F64": 5.47, "TRANS_F64": 17.
 SIMDS, CLOCK_GHZ = 1024, 2.4  # MI355X: 256 CUs x 4 SIMDs, peak engine clock
 
 
+def shard_time_prediction(n: int, m: int, family: str, shard_qps: int, total_qps: int):
+    """One-GPU kernel time of a `shard_qps` launch and of the whole batch, by
+    linear interpolation of the committed batch scan (profiles/batch_scan.json,
+    tools/batch_scan.py, box family at n = 16, m = 32), and the speed-up the
+    kernel alone allows: T(total) / T(shard).  None outside the scanned range."""
+    path = os.path.join(ROOT, "profiles", "batch_scan.json")
+    if (n, m, family) != (16, 32, "box") or not os.path.exists(path):
+        return None
+    scan = json.load(open(path))
+    pts = sorted((int(k[1:-3]), v) for k, v in scan.items() if k.startswith("B") and k.endswith("_us"))
+
+    def t_us(b):
+        for (b0, t0), (b1, t1) in zip(pts, pts[1:]):
+            if b0 <= b <= b1:
+                return t0 + (t1 - t0) * (b - b0) / (b1 - b0)
+        return None
+    ts, tt = t_us(shard_qps), t_us(total_qps)
+    if ts is None or tt is None:
+        return None
+    return {"shard_kernel_ms": ts * 1e-3, "total_kernel_ms": tt * 1e-3, "kernel_bound_speedup": tt / ts,
+            "source": "profiles/batch_scan.json (one GPU, kernel time vs batch)", "revision": scan.get("revision")}
+
+
 def valu_ceiling(traffic, waves: int, kern_ms: float):
     """The kernel's issue-rate bound: every VALU instruction class of the
     committed PMC pass (SQ_INSTS_VALU_FMA_F64 / _MUL_F64 / _ADD_F64 /
@@ -290,7 +313,7 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     import qpb
-    from qpb.dist import gather_results, max_over_ranks, shard
+    from qpb.dist import check_gathered, gather_results, max_over_ranks, shard
 
     dist_info = None
     if world > 1:
@@ -339,20 +362,38 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(e) for a, e in evs) / args.steps
+    local_step_ms = elapsed / args.steps * 1e3
     elapsed = max_over_ranks(elapsed, device)
+    if dist_info is not None:
+        # per rank: its shard, its kernel time (HIP events on its launch stream)
+        # and its own step time, beside the one-GPU kernel-time prediction for a
+        # shard of that size (profiles/batch_scan.json): a speed-up short of N
+        # then reads as the kernel's per-launch fixed cost, not communication
+        mine = {"rank": rank, "shard_first": start, "shard_qps": B, "kernel_ms": kern_ms,
+                "step_ms": local_step_ms}
+        per = [None] * world
+        dist.all_gather_object(per, mine)
+        dist_info["per_rank"] = per
+        pred = shard_time_prediction(n, m, args.family, B, total_B)
+        if pred:
+            dist_info["single_gpu_prediction"] = pred
     gather_ms, gather = None, None
     if args.gather and world > 1:  # the trivial result gather of SURVEY.md §8e, outside the timed steps
         barrier()
         tg = time.perf_counter()
-        full = gather_results({"x": sol.x, "lam": sol.lam, "active": sol.active, "status": sol.status}, total_B)
+        local = {"x": sol.x, "lam": sol.lam, "active": sol.active, "status": sol.status}
+        full = gather_results(local, total_B)
         barrier()
         gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, device)
+        # every rank's exact shard digest against its rows of the gathered batch
+        # (qpb.dist.check_gathered; after the timed gather), every status a valid code
+        digests_ok = check_gathered(full, local, total_B)
         if rank == 0:
-            # rank 0 holds the whole batch: its own shard in place, every status a valid code
-            checked = bool(full["x"].shape[0] == total_B and torch.equal(full["x"][start:start + B], sol.x)
+            checked = bool(full["x"].shape[0] == total_B and digests_ok
                            and ((full["status"] >= 0) & (full["status"] <= 4)).all())
             gather = {"dst": 0, "collective": "gather (x, lam, active, status) to rank 0",
-                      "bytes_per_qp": 8 * (n + m) + 4 * ((m + 31) // 32) + 4, "checked": checked}
+                      "bytes_per_qp": 8 * (n + m) + 4 * ((m + 31) // 32) + 4, "checked": checked,
+                      "check": "each rank's integer digest of its shard == the digest of its rows on rank 0"}
         del full
 
     # pipelined leg, outside the timed steps: K batches over S streams, each

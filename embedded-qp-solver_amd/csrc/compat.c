@@ -81,16 +81,14 @@ static void pool_release(void)
 
 void qpb_compat_init(unsigned n_dim, double admm_box_min, double admm_box_max)
 {
-	/* The reference packs N_DIM into 16 bits (matrix_type.h:14-17), but its
-	 * solvers run here on the GPU replicas (qpb_ref_solve), which take
-	 * n <= QPB_MAX_N: refuse such an N_DIM now, with the reason, instead of
-	 * failing inside the caller's first solve. */
-	if (n_dim == 0 || n_dim > QPB_MAX_N) {
-		fprintf(stderr,
-			"kmalloc_init: N_DIM = %u is outside 1..%d: the qp_solvers.h solvers of this library "
-			"(gradient_descent_with_line_search, newton_method_with_line_search, admm) run on the "
-			"batched GPU replicas, which take n <= %d (qpb.h QPB_MAX_N)\n",
-			n_dim, QPB_MAX_N, QPB_MAX_N);
+	/* The reference packs N_DIM into 16 bits (matrix_type.h:14-17): its host
+	 * matrix library (matrix_mult, matrix_invert, matrix_norm, the pools)
+	 * works at any N_DIM up to 65535, and so does this one.  Only the three
+	 * qp_solvers.h solvers run on the batched GPU replicas, which take
+	 * n <= QPB_MAX_N; they refuse a larger N_DIM with the reason (run_ref). */
+	if (n_dim == 0 || n_dim > 0xFFFFu) {
+		fprintf(stderr, "kmalloc_init: N_DIM = %u is outside 1..65535 (the 16-bit dimension fields of "
+				"struct _matrix, matrix_type.h)\n", n_dim);
 		exit(EXIT_FAILURE);
 	}
 	pool_release();
@@ -100,6 +98,13 @@ void qpb_compat_init(unsigned n_dim, double admm_box_min, double admm_box_max)
 #if !QPB_POOL_PER_SLOT
 	g_nxn_store = calloc((size_t)POOL_NXN * n_dim * n_dim, sizeof(double));
 	g_nx1_store = calloc((size_t)POOL_NX1 * n_dim, sizeof(double));
+	if (!g_nxn_store || !g_nx1_store) {
+		/* the reference's pools are static arrays sized by N_DIM: a size
+		 * that does not fit is fatal there too */
+		fprintf(stderr, "kmalloc_init: N_DIM = %u: the matrix pools (%d n x n, %d n x 1) do not fit in memory\n",
+			n_dim, POOL_NXN, POOL_NX1);
+		exit(EXIT_FAILURE);
+	}
 #endif
 	for (int i = 0; i < POOL_NXN; i++) {
 		g_nxn[i].used = 0;
@@ -486,6 +491,16 @@ struct _matrix *quadratic_form_eval_grad(struct _quadratic_form *qf, struct _mat
 /* ------------------------------------------------------------- solvers */
 static struct _matrix *run_ref(int mode, struct _matrix *x0, unsigned iterations, struct _quadratic_form *qf)
 {
+	if (MATRIX_GET_ROW(qf->p) > QPB_MAX_N) {
+		fprintf(stderr,
+			"%s: N_DIM = %u: the qp_solvers.h solvers of this library run on the batched GPU replicas "
+			"(qpb_ref_solve), which take n <= %d (qpb.h QPB_MAX_N); the matrix_ops.h routines have no "
+			"such limit\n",
+			mode == QPB_REF_GD ? "gradient_descent_with_line_search"
+					   : mode == QPB_REF_NEWTON ? "newton_method_with_line_search" : "admm",
+			(unsigned)MATRIX_GET_ROW(qf->p), QPB_MAX_N);
+		exit(EXIT_FAILURE); /* the reference exits on its fatal errors (qp_solvers.c:79-82) */
+	}
 	struct _matrix *x = matrix_alloc(Nx1);
 	if (!x)
 		return NULL;

@@ -717,11 +717,13 @@ size_t ref_lds_bytes(int n, bool with_p) {
 // cached workspace; `launch` queues the kernel while the cache is locked
 hipError_t ref_big_launch(long long batch, int n, size_t lds, hipStream_t stream,
                           const std::function<void(unsigned grid, double *ws)> &launch) {
-  int dev = 0, cus = 0;
+  int dev = 0, cus = 0, lds_cu = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  // the CU's LDS, from the device (160 KiB on gfx950)
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
   if (e != hipSuccess) return e;
-  long long per_cu = (long long)(160 * 1024 / lds);
+  long long per_cu = (long long)((size_t)lds_cu / lds);
   if (per_cu < 1) per_cu = 1;
   if (per_cu > qpb::REF_MAX_WG_PER_CU) per_cu = qpb::REF_MAX_WG_PER_CU;
   const long long slots = (long long)cus * per_cu;

@@ -127,7 +127,9 @@ def solve(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0, out
     """Batched min 1/2 x^T H x + f^T x s.t. A x <= b on the GPU (torch CUDA float64 tensors).
 
     H (B,n,n), f (B,n), A (B,m,n), b (B,m).  Asynchronous on ``stream``
-    (default: torch's current stream).  A/b omitted -> unconstrained solve.
+    (default: torch's current stream; the n > 32 class caches a scratch buffer per
+    stream: call ``release_stream_workspace(stream)`` before destroying a stream
+    passed here).  A/b omitted -> unconstrained solve.
     ``flags``: QPB_FLAG_DIAG_* kernel variants (measurement only, qpb.h).
     """
     import torch
@@ -242,7 +244,8 @@ def _require_f64_cuda(name: str, t, shape: tuple):
 
 def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), stream=None):
     """Reference-semantics batched solvers (qp_solvers.c replicas) on CUDA tensors:
-    P (B, n, n), q (B, n), x0 (B, n) or None (zeros)."""
+    P (B, n, n), q (B, n), x0 (B, n) or None: zeros for GD and Newton, unused
+    by ADMM (qp_solvers.c:256 ignores its x0)."""
     import torch
     if not (isinstance(q, torch.Tensor) and q.dim() == 2):
         raise ValueError("qpb.ref_solve: q must be a (B, n) tensor")
@@ -255,6 +258,10 @@ def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), s
             raise ValueError("qpb.ref_solve: P, q and x0 must be on one device")
     elif P.device != q.device:
         raise ValueError("qpb.ref_solve: P and q must be on one device")
+    elif mode != REF_ADMM:
+        # GD and Newton start from x0 (qpb_ref_solve requires it); ADMM ignores
+        # it, as the reference does (qp_solvers.c:256)
+        x0 = torch.zeros_like(q)
     x = torch.empty((B, n), dtype=torch.float64, device=q.device)
     it = torch.empty((B,), dtype=torch.int32, device=q.device)
     d = RefDesc(n, mode, B, iterations, 0, float(box[0]), float(box[1]))
@@ -262,6 +269,26 @@ def ref_solve(mode: int, P, q, x0=None, *, iterations: int, box=(-1e12, 1e12), s
                             _ptr(x), _ptr(it), _stream_ptr(stream))
     _check(rc, "qpb_ref_solve")
     return x, it
+
+
+_lib.qpb_release_stream_workspace.argtypes = [_vp]
+_lib.qpb_release_stream_workspace.restype = ctypes.c_int
+_lib.qpb_release_workspaces.argtypes = []
+_lib.qpb_release_workspaces.restype = ctypes.c_int
+
+
+def release_stream_workspace(stream=None) -> None:
+    """qpb_release_stream_workspace: free the scratch buffer cached for
+    `stream` (a torch.cuda.Stream or ExternalStream; None = the current
+    stream).  The n <= 128 kernels and the reference replicas above n = 64
+    cache one buffer per (device, stream) and free it stream-ordered on that
+    stream, so call this before destroying a stream passed as ``stream=``."""
+    _check(_lib.qpb_release_stream_workspace(_stream_ptr(stream)), "qpb_release_stream_workspace")
+
+
+def release_workspaces() -> None:
+    """qpb_release_workspaces: synchronise every cached stream and free all the scratch buffers."""
+    _check(_lib.qpb_release_workspaces(), "qpb_release_workspaces")
 
 
 def matrix_invert(P, stream=None):

@@ -62,3 +62,43 @@ def gather_results(local: dict, total: int, dst: int | None = 0):
             dist.gather(pad, parts, dst=dst)
         out[key] = torch.cat([p[:c] for p, c in zip(parts, counts)], 0) if parts is not None else None
     return out if (dst is None or rank == dst) else None
+
+
+def shard_digest(local: dict) -> dict:
+    """Exact, summation-order-independent digest of a result shard (dict of
+    tensors with a leading batch dimension): per tensor, the integer sums of
+    the low and high 32 bits of every element's bit pattern and a
+    position-weighted sum of its low 16 bits (weights (i mod 65521) + 1), so a
+    corrupted, missing or misplaced element changes it.  Integer sums do not
+    depend on the reduction order, so a shard and the same rows of a gathered
+    batch give equal digests whatever their alignment."""
+    import torch
+    out = {}
+    for key, t in local.items():
+        v = t.contiguous().reshape(-1)
+        if v.element_size() == 8:
+            v = v.view(torch.int64)
+        else:
+            v = v.view(torch.int32).to(torch.int64)
+        lo, hi = v & 0xFFFFFFFF, (v >> 32) & 0xFFFFFFFF
+        w = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 65521 + 1
+        out[key] = (int(lo.sum()), int(hi.sum()), int(((v & 0xFFFF) * w).sum()), int(v.numel()))
+    return out
+
+
+def check_gathered(full: dict, local: dict, total: int) -> bool:
+    """Every rank's shard digest equals the digest of its rows of the batch
+    gathered to rank 0 (`full`, None on the other ranks).  Collective: every
+    rank calls it; the answer is meaningful on the rank that holds `full`."""
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    mine = shard_digest(local)
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    if full is None:
+        return True
+    for r, d in enumerate(every):
+        start, count = shard(total, r, world)
+        if d != shard_digest({k: full[k][start:start + count] for k in local}):
+            return False
+    return True

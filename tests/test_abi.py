@@ -118,3 +118,16 @@ def _device_present():
 def test_python_binding_imports():
     import qpb
     assert qpb.version().startswith("qpb")
+
+
+def test_version_macros_match_library():
+    """include/qpb.h's QPB_VERSION_MAJOR / _MINOR name the library they ship
+    with: qpb_version() reports "qpb MAJOR.MINOR (...)"."""
+    src = open(HEADERS[0]).read()
+    major = int(re.search(r"#define QPB_VERSION_MAJOR (\d+)", src).group(1))
+    minor = int(re.search(r"#define QPB_VERSION_MINOR (\d+)", src).group(1))
+    lib = ctypes.CDLL(LIB)
+    lib.qpb_version.restype = ctypes.c_char_p
+    m = re.match(r"qpb (\d+)\.(\d+) \(", lib.qpb_version().decode())
+    assert m, lib.qpb_version()
+    assert (int(m.group(1)), int(m.group(2))) == (major, minor)

@@ -142,27 +142,51 @@ def test_reference_main_builds_against_compat():
     assert os.access(path, os.X_OK)
 
 
-@pytest.mark.parametrize("n_dim,ok", [(128, True), (129, False), (0, False), (65535, False)])
-def test_compat_init_rejects_ndim_beyond_the_solvers(n_dim, ok):
-    """kmalloc_init() (qpb_compat_init) refuses an N_DIM the GPU solver
-    replicas cannot take, with the reason, at init -- not by exit() inside the
-    caller's first solve.  A child process: the refusal exits, as the
-    reference exits on its own fatal errors (qp_solvers.c:79-82).  Under
-    tests/test_sanitizers.py this runs against the ASan/UBSan build."""
+def _child(code):
     import subprocess
     import sys
-    code = ("import ctypes, os\n"
-            "L = ctypes.CDLL(os.environ['QPB_LIB_UNDER_TEST'])\n"
-            "L.qpb_compat_init.argtypes = [ctypes.c_uint, ctypes.c_double, ctypes.c_double]\n"
-            f"L.qpb_compat_init({n_dim}, -1e12, 1e12)\n"
-            "L.matrix_alloc.restype = ctypes.c_void_p\n"
-            "print('alloc', bool(L.matrix_alloc(0)))\n")
     env = dict(os.environ, QPB_LIB_UNDER_TEST=LIB)
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    pre = ("import ctypes, os\n"
+           "L = ctypes.CDLL(os.environ['QPB_LIB_UNDER_TEST'])\n"
+           "L.qpb_compat_init.argtypes = [ctypes.c_uint, ctypes.c_double, ctypes.c_double]\n"
+           "L.matrix_alloc.restype = ctypes.c_void_p\n")
+    return subprocess.run([sys.executable, "-c", pre + code], env=env, capture_output=True, text=True, timeout=120)
+
+
+@pytest.mark.parametrize("n_dim,ok", [(128, True), (129, True), (300, True), (0, False), (65536, False)])
+def test_compat_init_accepts_the_reference_dimension_range(n_dim, ok):
+    """kmalloc_init() (qpb_compat_init) takes any N_DIM the reference's 16-bit
+    dimension fields hold (matrix_type.h:14-17): the host matrix library works
+    there (an n x n product at N_DIM = 300 below); 0 and 65 536 are refused with
+    the reason.  A child process: the refusal exits, as the reference exits on
+    its own fatal errors (qp_solvers.c:79-82).  Under tests/test_sanitizers.py
+    this runs against the ASan/UBSan build."""
+    r = _child(f"L.qpb_compat_init({n_dim}, -1e12, 1e12)\n"
+               "a, b, c = (ctypes.c_void_p(L.matrix_alloc(0)) for _ in range(3))\n"
+               "print('alloc', bool(a.value and b.value and c.value))\n"
+               "L.matrix_mult(c, a, b)\n"
+               "print('mult ok')\n")
     if ok:
         assert r.returncode == 0, r.stderr
-        assert "alloc True" in r.stdout
+        assert "alloc True" in r.stdout and "mult ok" in r.stdout
     else:
         assert r.returncode != 0
-        assert f"N_DIM = {n_dim} is outside 1..128" in r.stderr
+        assert f"N_DIM = {n_dim} is outside 1..65535" in r.stderr
         assert "alloc" not in r.stdout
+
+
+@pytest.mark.parametrize("solver", ["admm", "newton_method_with_line_search", "gradient_descent_with_line_search"])
+def test_compat_solvers_refuse_ndim_beyond_the_gpu_replicas(solver):
+    """At N_DIM = 129 the qp_solvers.h solvers (GPU replicas, n <= 128) exit
+    with the reason before any device call; the matrix routines kept working."""
+    r = _child("L.qpb_compat_init(129, -1e12, 1e12)\n"
+               "L.quadratic_form_alloc.restype = ctypes.c_void_p\n"
+               "L.quadratic_form_alloc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double]\n"
+               "p, q, x = (ctypes.c_void_p(L.matrix_alloc(t)) for t in (0, 1, 1))\n"
+               "qf = ctypes.c_void_p(L.quadratic_form_alloc(p, q, 0.0))\n"
+               f"L.{solver}.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]\n"
+               f"L.{solver}(x, 1, qf)\n"
+               "print('returned')\n")
+    assert r.returncode != 0
+    assert "returned" not in r.stdout
+    assert f"{solver}: N_DIM = 129" in r.stderr and "n <= 128" in r.stderr

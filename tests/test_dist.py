@@ -75,3 +75,43 @@ def test_two_rank_shard_solve_gather(total):
     for r in range(2):  # the all-gather form gives every rank the same batch
         assert np.array_equal(ret[f"every_{r}_x"], ref)
         assert np.array_equal(ret[f"every_{r}_lam"], ret["lam"])
+
+
+def _digest_worker(rank, world, port, ret):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qpb.dist import check_gathered, gather_results, shard as sh
+    total = 11
+    start, count = sh(total, rank, world)
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(total, 4, generator=g, dtype=torch.float64)
+    S = torch.arange(total, dtype=torch.int32)
+    local = {"x": X[start:start + count].clone(), "status": S[start:start + count].clone()}
+    full = gather_results(local, total)
+    ret[f"ok_{rank}"] = check_gathered(full, local, total)
+    # rank 0 corrupts one element of rank 1's rows, then swaps two of its own rows
+    if rank == 0:
+        full["x"].view(torch.int64)[start + count, 2] ^= 1  # the lowest mantissa bit
+    ret[f"bad_{rank}"] = check_gathered(full, local, total)
+    if rank == 0:
+        full["x"].view(torch.int64)[start + count, 2] ^= 1
+        full["x"][[0, 1]] = full["x"][[1, 0]]
+    ret[f"swap_{rank}"] = check_gathered(full, local, total)
+    dist.destroy_process_group()
+
+
+def test_gather_check_digests_catch_corruption_and_misplacement():
+    """qpb.dist.check_gathered (bench.py --gather's check): every rank's exact
+    integer digest of its shard against its rows of the batch gathered to rank
+    0 -- equal for a correct gather, unequal for one flipped low bit in another
+    rank's rows and for two swapped rows."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_digest_worker, args=(2, port, ret), nprocs=2, join=True)
+    assert ret["ok_0"] is True and ret["ok_1"] is True
+    assert ret["bad_0"] is False and ret["bad_1"] is True  # only rank 0 holds the batch
+    assert ret["swap_0"] is False

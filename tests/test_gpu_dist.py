@@ -88,6 +88,14 @@ def test_bench_gpus_2_runs_two_ranks(qpb):
     assert sorted(x["rank"] for x in d["ranks"]) == [0, 1]
     assert line["gather_ms"] is not None and line["gather_ms"] >= 0.0
     assert line["gather"]["checked"] is True
+    # per rank: its shard, its own kernel time (HIP events) and step time, and
+    # the one-GPU prediction for a launch of that shard size
+    per = sorted(d["per_rank"], key=lambda x: x["rank"])
+    assert [(x["shard_first"], x["shard_qps"]) for x in per] == [(0, 4096), (4096, 4096)]
+    assert all(x["kernel_ms"] > 0.0 and x["step_ms"] >= x["kernel_ms"] * 0.5 for x in per)
+    pred = d["single_gpu_prediction"]
+    assert pred["shard_kernel_ms"] > 0.0 and pred["total_kernel_ms"] > pred["shard_kernel_ms"]
+    assert 1.0 < pred["kernel_bound_speedup"] <= 2.0
     # the pipelined leg (two streams per rank, max over ranks) gives the same answers
     pl = line["pipelined"]
     assert pl["streams"] == 2 and pl["answers_equal"] is True and pl["value"] > 0.0

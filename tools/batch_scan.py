@@ -27,8 +27,8 @@ def main():
     fam = os.environ.get("FAM", "box")
     out = {}
     bs = os.environ.get("BS")
-    sizes = [int(x) for x in bs.split(",")] if bs else [4096, 12288, 24576, 36864, 49152, 61440, 65536, 73728,
-                                                         98304, 131072, 196608, 262144]
+    sizes = [int(x) for x in bs.split(",")] if bs else [4096, 8192, 16384, 32768, 65536, 131072, 262144,
+                                                         524288, 1048576]
     Bmax = max(sizes + [262144])
     H, f, A, b = qpb.generate(16, Bmax, 1, family=fam, shift=1.0, box=10.0, device=dev)
     for B in sizes:
@@ -42,6 +42,17 @@ def main():
         sol = qpb.solve(h, ff, a, bb)
         ms = t_kernel(lambda: qpb.lib().qpb_solve(*_diag_args(h, ff, a, bb, sol, 16)))
         out[f"mall_B{B}_us"] = round(ms * 1e3, 1)
+    # the revision of the kernel scanned (bench.py's shard-time prediction reads it)
+    out["revision"] = sorted(r for r in bench.kernel_revisions(qpb.version()) if r.startswith("gi_dense"))[0]
+    big = sorted(B for B in sizes if B >= 131072)
+    if len(big) >= 2:
+        # T(B) = a + c B over the large batches: a = the per-launch fixed cost
+        import numpy as np
+        t = np.array([out[f"B{B}_us"] for B in big])
+        c, a = np.polyfit(np.array(big, dtype=float), t, 1)
+        out["fit_intercept_us"], out["fit_ns_per_qp"] = float(a), float(c * 1e3)
+    if "B131072_us" in out and "B1048576_us" in out:
+        out["T1M_over_T131072"] = out["B1048576_us"] / out["B131072_us"]
     print(json.dumps(out, indent=1))
 
 
