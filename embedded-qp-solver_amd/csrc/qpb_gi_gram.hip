@@ -58,14 +58,18 @@ constexpr int NBUF = 2136;
 constexpr int OFF_TRI = 0;
 constexpr int OFF_ROWS = LP;  // diagonal-tile inverses (setup) / D_W rows (loop)
 constexpr int OFF_BUF = LDS_D - NBUF;
+// Q1 rows in LDS at stride QS: 2 QS = 32 mod 64 dwords, so the row-adjacent
+// lane groups of one b64 read (the d and w phases) hit opposite bank halves
+constexpr int QS = 144;
+constexpr int QL = (OFF_BUF - OFF_ROWS) / QS;  // Q1 rows in LDS (70)
 // Permuted vectors (u, w, y) keep lane group g's 32 entries at 34 g: the four
 // groups' b128 reads then start 4 banks apart instead of on the same banks.
 constexpr int B_CAND = OFF_BUF;                // per wave: its most violated row of D (PV each)
 constexpr int B_CSP = B_CAND + NWV * PV;       // per wave: that row's slack
-constexpr int B_W = B_CSP + NWV;               // (round 4's w; unused since v5)
+constexpr int B_W = B_CSP + NWV;               // w (padded permuted)
 constexpr int B_V = B_W + PV;                  // per-wave candidate row norms (NWV) and DROP scratch (row k of Z, at NB); lambda scatter at the end
 constexpr int B_R = B_V + MB;                  // r by position
-constexpr int B_CB = B_R + NB;                 // (round 4's d = Q1 u; unused since v5)
+constexpr int B_CB = B_R + NB;                 // d = Q1 u by position
 constexpr int B_LAM = B_CB + NB;               // multipliers by position
 constexpr int B_Y = B_LAM + NB;                // y (padded permuted), then y + D_W^T lam
 constexpr int B_RED = B_Y + PV;                // selection keys, partial reductions, scalars
@@ -81,12 +85,9 @@ static_assert(OFF_ROWS + 8 * LIT <= OFF_BUF, "diagonal-tile inverses fit the row
 // B_RED slots
 constexpr int R_KEY = 0;    // per-wave selection keys (NWV)
 constexpr int R_T1 = 8;     // per-wave (ratio min, argmin position) pairs (2 NWV)
+constexpr int R_ND2 = 24;   // per-wave partial |w|^2 (NWV)
 constexpr double kDepTol = 1e-24;
-// loop: each wave's DROP block (32 rows x 17 doubles) from OFF_ROWS, then
-// |D[row,:]|^2 by row (the rows area is free once the setup is done)
-constexpr int DN2S = OFF_ROWS + NWV * 32 * 17;
-static_assert(DN2S + MB <= OFF_BUF, "loop scratch fits the rows area");
-constexpr long long SCRATCH = LP;  // doubles per workgroup: L, kept for the final solves
+constexpr long long SCRATCH = LP + (long long)(NB - QL) * NB;  // doubles per workgroup
 
 using d4 = __attribute__((__vector_size__(4 * sizeof(double)))) double;
 
@@ -414,6 +415,13 @@ __device__ __forceinline__ void solve_upper(const double *Lp, int nb, int l, dou
   a1 *= id1;
 }
 
+// ------------------------------------------------------- Q1 row storage
+struct Rows {
+  double *lds;  // rows 0..QL-1, stride QS
+  double *gl;   // rows QL.. (per-workgroup global scratch), stride NB
+  __device__ __forceinline__ double *row(int j) const { return j < QL ? lds + j * QS : gl + (j - QL) * NB; }
+};
+
 // ------------------------------------------------------------------ kernel
 template <bool STAMP>
 __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
@@ -428,12 +436,13 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
   SectionClock<STAMP> clk;
   double *Lp = lds + OFF_TRI;  // L, then Z = R^{-1} (packed by columns)
   double *LI = lds + OFF_ROWS;
-  double *vb = lds + B_V, *rb = lds + B_R, *lamb = lds + B_LAM, *yb = lds + B_Y;
+  double *wb = lds + B_W, *vb = lds + B_V, *rb = lds + B_R, *lamb = lds + B_LAM, *yb = lds + B_Y;
   double *red = lds + B_RED;
   int *flags = reinterpret_cast<int *>(lds + B_INT);
   int *iamb = reinterpret_cast<int *>(lds + B_IAM);
   // per-workgroup scratch: L (packed), then the Q1 rows past QL
   double *Lgl = scratch + (long long)blockIdx.x * SCRATCH;
+  const Rows QR{lds + OFF_ROWS, Lgl + LP};
   const int T = (n + 15) >> 4, nb = 16 * T;
   for (;;) {
     // lane ids re-derived opaquely per QP: lane-dependent values are not
@@ -560,8 +569,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     clk.tick(1);
     // |D[row,:]|^2 of the lane's rows (the dependency test's scale, published
     // with the selection key: no |u|^2 reduction in the loop)
-    // (kept by row in LDS, DN2S: registers are the loop's scarce resource)
-    double *dn2s = lds + DN2S;
+    double dn2[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       double a0 = 0.0, a1 = 0.0;
@@ -572,8 +580,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         a0 = __builtin_fma(E[t][k][2], E[t][k][2], a0);
         a1 = __builtin_fma(E[t][k][3], E[t][k][3], a1);
       }
-      const double v = group_sum(a0 + a1);
-      if (lk == 0) dn2s[row[t]] = v;
+      dn2[t] = group_sum(a0 + a1);
     }
     double invn[RT], thr[RT], s[RT];
     bool zero_bad = false, act[RT];
@@ -599,30 +606,27 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     bool done = status != QPB_MAX_ITER;
     clk.tick(2);
     // ------------------------------------------------------- active set
-    // G-I in the rotated basis (v5): D = A L^{-T} Q is kept in the registers,
-    // Q orthogonal, so that the rows W_j of the active constraints are zero on
-    // the free columns q..nb-1 and D[W_j, i] = R[i][j] (R upper triangular,
-    // kept as its inverse Z = R^{-1}, packed by columns in the triangle: Z[i][j]
-    // at tri(j, i)).  For the selected row u = D[p,:]:
-    //   d1 = u[:q], d2 = u[q:]        (G-I's J1^T n+, J2^T n+: no pass at all)
-    //   r = Z d1, |d2|^2, D d2        (one phase: the dual direction, the
-    //                                  partial step's ratio test, the slack
-    //                                  direction; every wave reads u itself)
-    //   ADD: one Householder reflection H = I - beta v v^T on the free columns
-    //        of every row (v = d2 + alpha e_q, alpha = sign(u_q)|d2|: row p's
-    //        free part becomes -alpha e_q), R gains the column (d1; -alpha) and
-    //        Z the column [-r; 1] / (-alpha) (the bordered inverse)
-    //   DROP k: Givens rotations on Z's columns (j, j+1), j = k .. q-2, chosen
-    //        to zero row k of Z; the same rotations on D's columns k .. q-1
-    //        (each wave its own rows, through LDS); row k of Z goes.
-    // Round 4's form kept D0 = A L^{-T} fixed and the active set as Q1's rows:
-    // d = Q1 u and w = u - Q1^T d were two more barrier-separated passes per
-    // iteration.  x is recovered from the multipliers: x = -H^{-1}(f + A^T lam),
-    // the active rows of A re-read (D0 is no longer in the registers).
+    // G-I's J = L^{-T} [Q1^T Q2] in the form D_W^T = Q1^T R, with R kept as
+    // its inverse Z = R^{-1}: the orthonormal rows Q1 (q x n, permuted column
+    // order; LDS rows at stride QS, rows past QL in the scratch) and the upper
+    // triangular Z (q x q, packed by columns in the triangle: Z[i][j] at
+    // tri(j, i)), positions 0 .. q-1 in the order of the active set.  For the
+    // selected row u = D[p,:] one iteration is
+    //   d = Q1 u                        (G-I's d1 = J1^T n+)
+    //   w = u - Q1^T d, |w|^2, r = Z d  (J2 J2^T n+, |d2|^2, R^{-1} d1; one
+    //                                    phase: w and r do not wait for each other)
+    //   D w, the step; ADD: Q1 gains the row w / |w|, Z the column
+    //   [-r / |w|; 1 / |w|] (the bordered inverse); DROP k: Givens rotations
+    //   on Z's columns j, j+1 (j = k .. q-2) chosen to zero row k of Z, the
+    //   same rotations on Q1's rows, then row k of Z and the last column and
+    //   row go (R with column k removed, re-triangularised, inverted).
+    // Every phase is a parallel pass: nothing is O(q^2) per ADD, and no
+    // triangular solve runs in the loop.
     int it = 0, p = 0, q = 0;
     bool selecting = true;
     double up = 0.0, dd = 0.0;
-    const double *ub = lds + B_CAND;  // u = D[p,:] (permuted, padded), written by the wave holding row p
+    const double *ub = lds + B_CAND;  // u = D[p,:]: the winning wave's candidate row
+    double *db = lds + B_CB;          // d by position
     // each wave offers its most violated row: the key (normalised slack, row
     // in the low mantissa bits) and its slack
     auto publish_key = [&]() {
@@ -641,24 +645,14 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         for (int t = 0; t < RT; ++t)
           if (row[t] == pw && lk == 0) {
             lds[B_CSP + wv] = s[t];
-            vb[wv] = dn2s[row[t]];  // B_V is free during the loop below NB
+            vb[wv] = dn2[t];  // B_V is free during the loop below NB
           }
       }
     };
-    // row p of the wave's registers -> u (the lanes holding it write their 32 entries each)
-    auto write_u = [&](int pr) {
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-        if (row[t] == pr) {
-          double *dst = lds + B_CAND + 34 * lk;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            *reinterpret_cast<double2 *>(&dst[4 * k]) = make_double2(E[t][k][0], E[t][k][1]);
-            *reinterpret_cast<double2 *>(&dst[4 * k + 2]) = make_double2(E[t][k][2], E[t][k][3]);
-          }
-        }
-    };
-    if (tid < NB) iamb[tid] = -1;
+    if (tid < NB) {
+      iamb[tid] = -1;
+      db[tid] = 0.0;
+    }
     if (!done) publish_key();
     __syncthreads();
     while (!done && it < max_iter) {
@@ -680,65 +674,105 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
         p = key_index256(kmin);
         up = 0.0;
         selecting = false;
-        if (wv == p / (16 * RT)) write_u(p);
+        // u = D[p,:] from the one wave that holds row p
+        if (wv == p / (16 * RT)) {
+#pragma unroll
+          for (int t = 0; t < RT; ++t)
+            if (row[t] == p) {
+              double *dst = lds + B_CAND + 34 * lk;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                *reinterpret_cast<double2 *>(&dst[4 * k]) = make_double2(E[t][k][0], E[t][k][1]);
+                *reinterpret_cast<double2 *>(&dst[4 * k + 2]) = make_double2(E[t][k][2], E[t][k][3]);
+              }
+            }
+        }
         __syncthreads();
-        // |u|^2 (the dependency test's scale; invariant under Q), published with the key
+        // |u|^2 (the dependency test's scale), published with the key
         dd = vb[p / (16 * RT)];
       }
       clk.tick(3);
-      const int qs = __builtin_amdgcn_readfirstlane(q);  // the same on every lane: a scalar
-      // ---- this lane's two entries of u (lane j of group lk: block entries
-      // 2j, 2j + 1, i.e. columns c0 = 16 (j >> 1) + lk + 8 (j & 1) and c0 + 4),
-      // the free part d2 (columns >= q) and |d2|^2, the same on every wave
-      const double2 uu = *reinterpret_cast<const double2 *>(&ub[34 * lk + 2 * li]);
-      const int c0 = 16 * (li >> 1) + lk + 8 * (li & 1), c1 = c0 + 4;
-      const double f0 = c0 >= qs ? uu.x : 0.0, f1 = c1 >= qs ? uu.y : 0.0;
-      const double nd2 = group_sum(row_sum(__builtin_fma(f0, f0, f1 * f1)));
-      // ---- slack direction D d2 (row products against the masked u)
-      double ds[RT];
-      {
-        double a[RT][4];
+      // ---- d = Q1 u: lane (lk, li) of wave w takes position 32 j + 4 w + lk
+      // over the columns li + 16 i (row sums over the 16 lanes finish it)
+      for (int t0 = 4 * wv; t0 < q; t0 += 4 * NWV) {
+        const int t = t0 + lk;
+        const int tt = t < q ? t : t0;
+        // all eight Q1 entries and u entries in flight before the FMAs; rows
+        // in LDS (the usual case, wave-uniform test) are read as LDS, not
+        // through generic pointers (flat loads, each waited for)
+        double qv[8], uv[8];
+        if (t0 + 3 < QL) {
+          const __attribute__((address_space(3))) double *qr =
+              (const __attribute__((address_space(3))) double *)(QR.lds + tt * QS);
 #pragma unroll
-        for (int t = 0; t < RT; ++t)
+          for (int i = 0; i < 8; ++i) qv[i] = qr[li + 16 * i];
+        } else {
+          const double *qr = QR.row(tt);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) a[t][r] = 0.0;
-        dpp_ready(f0);
-        dpp_ready(f1);
-        unroll<8>([&](auto K) {
-          constexpr int k = K;
+          for (int i = 0; i < 8; ++i) qv[i] = qr[li + 16 * i];
+        }
 #pragma unroll
-          for (int t = 0; t < RT; ++t) {
-            fmac_bc<2 * k>(a[t][0], f0, E[t][k][0]);
-            fmac_bc<2 * k>(a[t][1], f1, E[t][k][1]);
-            fmac_bc<2 * k + 1>(a[t][2], f0, E[t][k][2]);
-            fmac_bc<2 * k + 1>(a[t][3], f1, E[t][k][3]);
-          }
-        });
+        for (int i = 0; i < 8; ++i) uv[i] = ub[pad(li + 16 * i)];
+        double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-        for (int t = 0; t < RT; ++t) ds[t] = group_sum((a[t][0] + a[t][1]) + (a[t][2] + a[t][3]));
+        for (int i = 0; i < 8; i += 2) {
+          a0 = __builtin_fma(qv[i], uv[i], a0);
+          a1 = __builtin_fma(qv[i + 1], uv[i + 1], a1);
+        }
+        const double dv = row_sum(a0 + a1);
+        if (li == 0 && t < q) db[t] = dv;
       }
-      // ---- r = Z d1 over rows i = 16 w + li (lane group lk: the columns
-      // c >= i, c = lk mod 4; d1_c = u_c at 34 (c & 3) + (c >> 2)), then each
-      // wave's ratio minimum (first position at the minimum; waves in position order)
+      __syncthreads();
+      clk.tick(4);
+      // ---- w = u - Q1^T d: lane (lk, li) of wave w takes (permuted) column
+      // 16 w + li over the positions j = lk mod 4; |w|^2 per wave
+      {
+        const int c = 16 * wv + li;
+        double acc0 = 0.0, acc1 = 0.0;
+        const int qa = q < QL ? q : QL;
+        int j = lk;
+        // four positions per step, their eight reads in flight together
+        for (; j + 12 < qa; j += 16) {
+          const double d0 = db[j], d1 = db[j + 4], d2 = db[j + 8], d3 = db[j + 12];
+          const double q0 = QR.lds[j * QS + c], q1 = QR.lds[(j + 4) * QS + c];
+          const double q2 = QR.lds[(j + 8) * QS + c], q3 = QR.lds[(j + 12) * QS + c];
+          acc0 = __builtin_fma(d0, q0, acc0);
+          acc1 = __builtin_fma(d1, q1, acc1);
+          acc0 = __builtin_fma(d2, q2, acc0);
+          acc1 = __builtin_fma(d3, q3, acc1);
+        }
+        for (; j + 4 < qa; j += 8) {
+          acc0 = __builtin_fma(db[j], QR.lds[j * QS + c], acc0);
+          acc1 = __builtin_fma(db[j + 4], QR.lds[(j + 4) * QS + c], acc1);
+        }
+        if (j < qa) acc0 = __builtin_fma(db[j], QR.lds[j * QS + c], acc0);
+        for (j = QL + lk; j < q; j += 4) acc1 = __builtin_fma(db[j], QR.gl[(j - QL) * NB + c], acc1);
+        const double w = ub[pad(c)] - group_sum(acc0 + acc1);
+        if (lk == 0) wb[pad(c)] = w;
+        const double ws = wave_sum(lk == 0 ? w * w : 0.0);
+        if (l == 0) red[R_ND2 + wv] = ws;
+      }
+      // ---- r = Z d over rows i = 16 w + li (lane group lk: the columns
+      // c >= i, c = lk mod 4), then each wave's ratio minimum (first position
+      // at the minimum; waves in position order)
       {
         const int i = 16 * wv + li;
         double ratio = kBig;
-        if (16 * wv < qs) {
+        if (16 * wv < q) {
           double acc = 0.0, acc1 = 0.0;
           int c = lk + ((i > lk) ? ((i - lk + 3) & ~3) : 0);
-          const double *du = ub + 34 * lk;
           // four columns per step, their eight reads in flight together
-          for (; c + 12 < qs; c += 16) {
+          for (; c + 12 < q; c += 16) {
             const double z0 = Lp[tri(c, i)], z1 = Lp[tri(c + 4, i)], z2 = Lp[tri(c + 8, i)], z3 = Lp[tri(c + 12, i)];
-            const double d0 = du[c >> 2], d1 = du[(c >> 2) + 1], d2 = du[(c >> 2) + 2], d3 = du[(c >> 2) + 3];
+            const double d0 = db[c], d1 = db[c + 4], d2 = db[c + 8], d3 = db[c + 12];
             acc = __builtin_fma(z0, d0, acc);
             acc1 = __builtin_fma(z1, d1, acc1);
             acc = __builtin_fma(z2, d2, acc);
             acc1 = __builtin_fma(z3, d3, acc1);
           }
-          for (; c < qs; c += 4) acc = __builtin_fma(Lp[tri(c, i)], du[c >> 2], acc);
+          for (; c < q; c += 4) acc = __builtin_fma(Lp[tri(c, i)], db[c], acc);
           const double rt = group_sum(acc + acc1);
-          if (i < qs) {
+          if (i < q) {
             if (lk == 0) rb[i] = rt;
             if (rt > 0.0) ratio = lamb[i] * rcp(rt);
           }
@@ -750,42 +784,18 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           red[R_T1 + 2 * wv + 1] = kpos;
         }
       }
-      // the reflection an ADD would take, computed here under the other
-      // chains of this phase: alpha = sign(u_q) |d2| (no cancellation in
-      // v_q = u_q + alpha), beta = 1 / (|d2|^2 + alpha u_q); every row takes
-      // D[r, q:] -= beta (D[r, q:] . v) v, D[r, q:] . v = (D d2)_r + alpha D[r, q].
-      // Column q of the lane's rows: lane group q & 3, register (q >> 4,
-      // (q >> 2) & 3); the other groups get it through the group sum.
-      double alpha, coef[RT];
-      {
-        const double uq = qs < NB ? ub[34 * (qs & 3) + (qs >> 2)] : 0.0;
-        const double nrm = __builtin_sqrt(nd2);
-        alpha = uq >= 0.0 ? nrm : -nrm;
-        const double beta = rcp(__builtin_fma(alpha, uq, nd2));
-        double dq[RT] = {0.0, 0.0};
-        const bool own = lk == (qs & 3);
-        switch (qs >> 2) {
-#define QPB_GRAM_COLQ(C)                                                \
-  case C:                                                               \
-    _Pragma("unroll") for (int t = 0; t < RT; ++t) dq[t] = own ? E[t][(C) >> 2][(C) & 3] : 0.0; \
-    break;
-          QPB_GRAM_COLQ(0) QPB_GRAM_COLQ(1) QPB_GRAM_COLQ(2) QPB_GRAM_COLQ(3) QPB_GRAM_COLQ(4) QPB_GRAM_COLQ(5)
-          QPB_GRAM_COLQ(6) QPB_GRAM_COLQ(7) QPB_GRAM_COLQ(8) QPB_GRAM_COLQ(9) QPB_GRAM_COLQ(10) QPB_GRAM_COLQ(11)
-          QPB_GRAM_COLQ(12) QPB_GRAM_COLQ(13) QPB_GRAM_COLQ(14) QPB_GRAM_COLQ(15) QPB_GRAM_COLQ(16) QPB_GRAM_COLQ(17)
-          QPB_GRAM_COLQ(18) QPB_GRAM_COLQ(19) QPB_GRAM_COLQ(20) QPB_GRAM_COLQ(21) QPB_GRAM_COLQ(22) QPB_GRAM_COLQ(23)
-          QPB_GRAM_COLQ(24) QPB_GRAM_COLQ(25) QPB_GRAM_COLQ(26) QPB_GRAM_COLQ(27) QPB_GRAM_COLQ(28) QPB_GRAM_COLQ(29)
-          QPB_GRAM_COLQ(30) QPB_GRAM_COLQ(31)
-#undef QPB_GRAM_COLQ
-        }
-#pragma unroll
-        for (int t = 0; t < RT; ++t) coef[t] = -beta * __builtin_fma(alpha, group_sum(dq[t]), ds[t]);
-      }
       // s_p, read before the barrier: an ADD's publish_key below rewrites the
       // candidate slacks while slower waves may still be in this step
       const double sp = lds[B_CSP + p / (16 * RT)];
       __syncthreads();
       clk.tick(5);
+      // ---- slack direction D w (issued before the scalar chain below needs it)
+      double ds[RT];
+      row_dot(E, wb + 34 * lk, ds);
       // ---- step lengths (identical arithmetic on every wavefront)
+      double nd2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) nd2 += red[R_ND2 + w];
       double t1 = kBig;
       int kdrop = 0;
 #pragma unroll
@@ -807,42 +817,22 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       }
       up += tt;
       clk.tick(16);
-      if (tid < qs) lamb[tid] = __builtin_fma(-tt, rb[tid], lamb[tid]);
+      if (tid < q) lamb[tid] = __builtin_fma(-tt, rb[tid], lamb[tid]);
       if (t2 <= t1) {
-        // ---- ADD p at position q: alpha = sign(u_q) |d2| (no cancellation in
-        // v_q = u_q + alpha), beta = 1 / (|d2|^2 + alpha u_q); every row takes
-        // D[r, q:] -= beta (D[r, q:] . v) v, with D[r, q:] . v = (D d2)_r + alpha D[r, q]
-        // u's pair (unchanged since phase A: u is rewritten only at a selection or a DROP)
-        const double2 ua = *reinterpret_cast<const double2 *>(&ub[34 * lk + 2 * li]);
-        const int a0 = 16 * (li >> 1) + lk + 8 * (li & 1), a1 = a0 + 4;
-        const double v0 = (a0 > qs ? ua.x : a0 == qs ? ua.x + alpha : 0.0);
-        const double v1 = (a1 > qs ? ua.y : a1 == qs ? ua.y + alpha : 0.0);
+        // ---- ADD p at position q
+        const double rn = rsq(nd2);  // 1 / |w|
+        if (tid < NB) QR.row(q)[tid] = wb[pad(tid)] * rn;
+        if (tid < q) Lp[tri(q, tid)] = -rb[tid] * rn;
+        if (tid == q) Lp[tri(q, q)] = rn;
+        if (tid == 0) {
+          iamb[q] = p;
+          lamb[q] = up;
+        }
 #pragma unroll
         for (int t = 0; t < RT; ++t)
           if (row[t] == p) act[t] = true;
-        q = qs + 1;
+        ++q;
         selecting = true;
-        publish_key();  // the keys need only the slacks: out before the reflection
-        dpp_ready(v0);
-        dpp_ready(v1);
-        unroll<8>([&](auto K) {
-          constexpr int k = K;
-#pragma unroll
-          for (int t = 0; t < RT; ++t) {
-            fmac_bc<2 * k>(E[t][k][0], v0, coef[t]);
-            fmac_bc<2 * k>(E[t][k][1], v1, coef[t]);
-            fmac_bc<2 * k + 1>(E[t][k][2], v0, coef[t]);
-            fmac_bc<2 * k + 1>(E[t][k][3], v1, coef[t]);
-          }
-        });
-        // R's new column (d1; -alpha) -> Z's new column [-r; 1] / (-alpha)
-        const double irho = -rcp(alpha);
-        if (tid < qs) Lp[tri(qs, tid)] = -rb[tid] * irho;
-        if (tid == qs) Lp[tri(qs, qs)] = irho;
-        if (tid == 0) {
-          iamb[qs] = p;
-          lamb[qs] = up;
-        }
       } else {
         // ---- DROP position k
         const int k = kdrop;
@@ -850,15 +840,15 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 #pragma unroll
         for (int t = 0; t < RT; ++t)
           if (row[t] == cdrop) act[t] = false;
-        // row k of Z (columns k .. q-1) copied aside: every wave's rotation
-        // chain reads it while wave 0 rewrites Z in place
+        // row k of Z (columns k .. q-1) copied aside: the rotation chains of
+        // waves 0-2 read it while wave 0 rewrites Z in place
         double *zrow = vb + NB;
-        if (tid >= k && tid < qs) zrow[tid] = Lp[tri(tid, k)];
+        if (tid >= k && tid < q) zrow[tid] = Lp[tri(tid, k)];
         __syncthreads();  // the multiplier update above and zrow, before the shift
         // Rotation j (j = k .. q-2) on the pair (j, j+1) zeroes Z[k][j]: with
-        // X_k = Z[k][k] and X_{j+1} = hypot(X_j, Z[k][j+1]), c_j = Z[k][j+1] /
-        // X_{j+1}, s_j = -X_j / X_{j+1}.  Every lane that applies rotations
-        // runs this scalar chain itself.
+        // X_k = Z[k][k] and X_{j+1} = hypot(X_j, Z[k][j+1]) (the carried
+        // entry of row k), c_j = Z[k][j+1] / X_{j+1}, s_j = -X_j / X_{j+1}.
+        // Every wave that applies rotations runs this scalar chain itself.
         if (wv == 0) {
           // Z's columns: lane l carries rows l and l + 64; row i > k moves to
           // i - 1 (row k goes).  Step j reads column j+1 and writes column j;
@@ -867,7 +857,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           double x0 = l <= k ? Lp[tri(k, l <= k ? l : 0)] : 0.0;  // rows' entries in column k
           double x1 = l + 64 <= k ? Lp[tri(k, l + 64 <= k ? l + 64 : 0)] : 0.0;
           double X = zrow[k];
-          for (int j = k; j < qs - 1; ++j) {
+          for (int j = k; j < q - 1; ++j) {
             const double z0 = l <= j + 1 ? Lp[tri(j + 1, l <= j + 1 ? l : 0)] : 0.0;
             const double z1 = l + 64 <= j + 1 ? Lp[tri(j + 1, l + 64 <= j + 1 ? l + 64 : 0)] : 0.0;
             const double zk = zrow[j + 1];
@@ -884,138 +874,99 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
             if (l != k && i0 <= j && l <= j + 1) Lp[tri(j, i0)] = n0;
             if (l + 64 != k && i1 <= j && l + 64 <= j + 1) Lp[tri(j, i1)] = n1;
           }
+        } else if (wv == 1 || wv == 2) {
+          // Q1's rows, one column per thread
+          const int c = tid - 64;
+          if (k < q - 1) {
+            double X = zrow[k];
+            double cur = QR.row(k)[c];
+            for (int j = k; j < q - 1; ++j) {
+              const double zk = zrow[j + 1];
+              const double nx = QR.row(j + 1)[c];
+              const double h = __builtin_sqrt(__builtin_fma(X, X, zk * zk));
+              const double ih = 1.0 / h;
+              const double cs = zk * ih, sn = -X * ih;
+              QR.row(j)[c] = __builtin_fma(cs, cur, sn * nx);
+              cur = __builtin_fma(-sn, cur, cs * nx);
+              X = h;
+            }
+          }
         } else if (wv == 3) {
           // positions k+1 .. q-1 move down by one (reads before writes: one
           // wave's DS instructions run in order)
           const double l0 = lamb[l + 1], l1 = lamb[l + 64 < NB - 1 ? l + 65 : NB - 1];
           const int i0 = iamb[l + 1], i1 = iamb[l + 64 < NB - 1 ? l + 65 : NB - 1];
           wave_lds_sync();
-          if (l >= k && l < qs - 1) {
+          if (l >= k && l < q - 1) {
             lamb[l] = l0;
             iamb[l] = i0;
-          } else if (l == qs - 1) {
+          } else if (l == q - 1) {
             lamb[l] = 0.0;
             iamb[l] = -1;
           }
-          if (l + 64 >= k && l + 64 < qs - 1) {
+          if (l + 64 >= k && l + 64 < q - 1) {
             lamb[l + 64] = l1;
             iamb[l + 64] = i1;
-          } else if (l + 64 == qs - 1) {
+          } else if (l + 64 == q - 1) {
             lamb[l + 64] = 0.0;
             iamb[l + 64] = -1;
           }
         }
-        // D's columns k .. q-1, the same rotations, on every wave's own 32 rows:
-        // 16-column tiles through a per-wave LDS block (row stride 17); lane
-        // row (0..31) runs the chain along the tile, carrying `cur`
-        if (k < qs - 1) {
-          double *blk = lds + OFF_ROWS + wv * (32 * 17);
-          const int rr = l & 31;  // the chain's row (lanes 32..63 repeat it; their stores are masked)
-          double X = zrow[k], cur = 0.0;
-          const int kc0 = k >> 4, kc1 = (qs - 1) >> 4;
-          for (int kc = kc0; kc <= kc1; ++kc) {
-            // the tile's 8 values of this lane (2 row tiles x r, column lk + 4 r)
-            // and the next tile's first column (the chain reads x_{16 kc + 16}:
-            // lane group 0, r = 0 of tile kc + 1) go to the wave's block
-            wave_lds_sync();
-            switch (kc) {
-#define QPB_GRAM_TILE(C)                                                                          \
-  case C:                                                                                         \
-    _Pragma("unroll") for (int t = 0; t < RT; ++t) {                                              \
-      _Pragma("unroll") for (int r = 0; r < 4; ++r) blk[(16 * t + li) * 17 + lk + 4 * r] = E[t][C][r]; \
-      if ((C) < 7 && lk == 0) blk[(16 * t + li) * 17 + 16] = E[t][(C) < 7 ? (C) + 1 : 7][0];    \
-    }                                                                                             \
-    break;
-              QPB_GRAM_TILE(0) QPB_GRAM_TILE(1) QPB_GRAM_TILE(2) QPB_GRAM_TILE(3)
-              QPB_GRAM_TILE(4) QPB_GRAM_TILE(5) QPB_GRAM_TILE(6) QPB_GRAM_TILE(7)
-#undef QPB_GRAM_TILE
-            }
-            wave_lds_sync();
-            double *br = blk + rr * 17;
-            const int base = 16 * kc;
-            if (kc == kc0) cur = br[k - base];
-            // steps c = k+1 .. q-1 that read x_c in this tile (c - base in 1 .. 16)
-            const int cs0 = k + 1 > base + 1 ? k + 1 : base + 1;
-            const int ce = qs - 1 < base + 16 ? qs - 1 : base + 16;
-            for (int c = cs0; c <= ce; ++c) {
-              const double xc = br[c - base];
-              const double zk = zrow[c];
-              const double h = __builtin_sqrt(__builtin_fma(X, X, zk * zk));
-              const double ih = 1.0 / h;
-              const double cs = zk * ih, sn = -X * ih;
-              const double nw = __builtin_fma(cs, cur, sn * xc);
-              cur = __builtin_fma(-sn, cur, cs * xc);
-              X = h;
-              if (l < 32) br[c - 1 - base] = nw;
-            }
-            // the last column takes the dropped direction
-            if (l < 32 && qs - 1 >= base && qs - 1 < base + 16) br[qs - 1 - base] = cur;
-            wave_lds_sync();
-            switch (kc) {
-#define QPB_GRAM_BACK(C)                                                                          \
-  case C:                                                                                         \
-    _Pragma("unroll") for (int t = 0; t < RT; ++t) _Pragma("unroll") for (int r = 0; r < 4; ++r) \
-        E[t][C][r] = blk[(16 * t + li) * 17 + lk + 4 * r];                                       \
-    break;
-              QPB_GRAM_BACK(0) QPB_GRAM_BACK(1) QPB_GRAM_BACK(2) QPB_GRAM_BACK(3)
-              QPB_GRAM_BACK(4) QPB_GRAM_BACK(5) QPB_GRAM_BACK(6) QPB_GRAM_BACK(7)
-#undef QPB_GRAM_BACK
-            }
-          }
-        }
-        q = qs - 1;
-        // p stays selected: its slack after the partial step, its rotated row
-        if (wv == p / (16 * RT)) {
+        --q;
 #pragma unroll
-          for (int t = 0; t < RT; ++t)
-            if (row[t] == p && lk == 0) lds[B_CSP + wv] = s[t];
-          write_u(p);
-        }
+        for (int t = 0; t < RT; ++t)  // p stays selected: its slack after the partial step
+          if (row[t] == p && lk == 0) lds[B_CSP + wv] = s[t];
       }
       clk.tick(17);
+      if (selecting) publish_key();
       clk.tick(18);
       __syncthreads();
       clk.tick(6);
     }
 
     // ------------------------------------------------------------ outputs
-    // full multiplier vector by row (vb), the active-set words
+    // full multiplier vector by row (vb), the active-set words,
+    // g = y + D_W^T lam = y + D^T lam_full: each wave sums its 32 rows of D
+    // weighted by their multipliers (16-lane row sums), the eight partial
+    // vectors are added per column
     for (int e = tid; e < MB; e += NT) vb[e] = 0.0;
     __syncthreads();
     if (tid < q && iamb[tid] >= 0) vb[iamb[tid]] = lamb[tid];
+    __syncthreads();
+    {
+      double lw[RT];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) lw[t] = vb[row[t]];
+      double *part = lds + OFF_ROWS + wv * PV;  // the Q1 rows are dead now
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double a = lw[0] * E[0][k][r];
+#pragma unroll
+          for (int t = 1; t < RT; ++t) a = __builtin_fma(lw[t], E[t][k][r], a);
+          a = row_sum(a);
+          if (li == 0) part[34 * lk + 4 * k + r] = a;  // permuted column order, padded
+        }
+    }
+    __syncthreads();
+    if (tid < NB) {
+      double gsum = yb[pad(tid)];
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) gsum += lds[OFF_ROWS + w * PV + pad(tid)];
+      yb[pad(tid)] = gsum;
+    }
     {
       uint32_t word = 0;
 #pragma unroll
       for (int t = 0; t < RT; ++t) word |= (uint32_t)(__ballot(act[t] && lk == 0) & 0xFFFFull) << (16 * t);
       if (l == 0) flags[2 + wv] = (int)word;  // rows 32 wv .. 32 wv + 31
     }
-    // g = f + A^T lam: the active rows of A re-read (the registers hold D in
-    // the rotated basis); thread (h, c) sums positions h mod 4 of column c,
-    // eight rows' loads in flight at a time, the four partial columns added in
-    // a fixed order
-    {
-      const int c = tid & (NB - 1), h = tid >> 7;
-      const int qa = q, cc = c < n ? c : n - 1;
-      double acc = 0.0;
-      for (int i0 = h; i0 < qa; i0 += 32) {
-        double av[8], lv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int i = i0 + 4 * u;
-          const int rw = i < qa ? iamb[i] : iamb[i0];
-          av[u] = Aq[(long long)rw * n + cc];
-          lv[u] = i < qa ? lamb[i] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = __builtin_fma(lv[u], c < n ? av[u] : 0.0, acc);
-      }
-      lds[OFF_ROWS + h * NB + c] = acc;  // the DROP blocks are dead now
-    }
     __syncthreads();
     for (int e = tid; e < m; e += NT) lamg[g * m + e] = vb[e];
     const int words = (m + 31) >> 5;
     if (tid < words) actg[g * words + tid] = (uint32_t)flags[2 + tid];
-    // x = -L^{-T} L^{-1} g: L again (the triangle held Z)
+    // x = -L^{-T} g: L again (the triangle held Z)
     bool finite = true;
     clk.tick(7);
     if (spd) {
@@ -1038,14 +989,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       __syncthreads();
       clk.tick(8);
       if (wv == 0) {
-        const double *gp = lds + OFF_ROWS;
-        double x0 = 0.0, x1 = 0.0;
-        if (l < n) x0 = fg[g * n + l] + ((gp[l] + gp[NB + l]) + (gp[2 * NB + l] + gp[3 * NB + l]));
-        if (l + 64 < n)
-          x1 = fg[g * n + l + 64] + ((gp[l + 64] + gp[NB + l + 64]) + (gp[2 * NB + l + 64] + gp[3 * NB + l + 64]));
-        solve_lower(Lp, nb, l, x0, x1);
-        x0 = -x0;
-        x1 = -x1;
+        double x0 = -yb[pad(perm(l))], x1 = -yb[pad(perm(l + 64))];
         solve_upper(Lp, nb, l, x0, x1);
         if (l < n) xg[g * n + l] = x0;
         if (l + 64 < n) xg[g * n + l + 64] = x1;
