@@ -35,6 +35,9 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
 extern "C" hipError_t qpb_launch_gi_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
                                         const double *ub, double *x, double *lam, uint32_t *active, int32_t *status,
                                         int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_wave_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
+                                             const double *ub, double *x, double *lam, uint32_t *active,
+                                             int32_t *status, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, const double *q,
                                      const double *x0, double *x, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_qf_eval(int n, long long batch, const double *P, const double *q, double r,
@@ -145,21 +148,23 @@ extern "C" int qpb_solve_box(const qpb_desc *d, const double *H, const double *f
   int rc = check_desc(d);
   if (rc) return rc;
   if (d->m != 2 * d->n) return fail(QPB_ERR_INVALID_ARG, "qpb_solve_box: m must be 2n (got n=%d m=%d)", d->n, d->m);
-  if (d->n > 16)
-    return fail(QPB_ERR_UNSUPPORTED, "qpb_solve_box: n=%d > 16 (pass A = [I; -I], b = [ub; -lb] to qpb_solve)", d->n);
+  if (d->n > 32)
+    return fail(QPB_ERR_UNSUPPORTED, "qpb_solve_box: n=%d > 32 (pass A = [I; -I], b = [ub; -lb] to qpb_solve)", d->n);
   if (d->batch == 0) return 0;
   if (!H || !f || !x || !lam || !active || !status)
     return fail(QPB_ERR_INVALID_ARG, "H, f, x, lam, active and status are required");
   rc = check_device();
   if (rc) return rc;
-  // four QPs per wavefront: at most 2^27 QPs per launch (2^32 work-items)
-  const long long n = d->n, w = (2 * n + 31) / 32, step = 1LL << 27;
+  // n <= 16: four QPs per wavefront (qpb_gi_box.hip), at most 2^27 QPs per
+  // launch (2^32 work-items); 16 < n <= 32: one QP per wavefront (the BOX
+  // instantiation of qpb_gi_wave.hip), 2^25
+  const long long n = d->n, w = (2 * n + 31) / 32, step = n <= 16 ? 1LL << 27 : 1LL << 25;
   for (long long k0 = 0; k0 < d->batch; k0 += step) {
     qpb_desc c = *d;
     c.batch = d->batch - k0 < step ? d->batch - k0 : step;
-    hipError_t e = qpb_launch_gi_box(&c, H + k0 * n * n, f + k0 * n, lb ? lb + k0 * n : lb, ub ? ub + k0 * n : ub,
-                                     x + k0 * n, lam + k0 * 2 * n, active + k0 * w, status + k0,
-                                     iters ? iters + k0 : iters, (hipStream_t)stream);
+    hipError_t e = (n <= 16 ? qpb_launch_gi_box : qpb_launch_gi_wave_box)(
+        &c, H + k0 * n * n, f + k0 * n, lb ? lb + k0 * n : lb, ub ? ub + k0 * n : ub, x + k0 * n, lam + k0 * 2 * n,
+        active + k0 * w, status + k0, iters ? iters + k0 : iters, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "qpb_solve_box launch");
   }
   return 0;
@@ -389,4 +394,4 @@ extern "C" const char *qpb_last_error(void) { return g_err; }
 
 // the hot kernel revision is part of the string: profiles/pmc_traffic.json is
 // only trusted for the revision it was measured on (bench.py)
-extern "C" const char *qpb_version(void) { return "qpb 0.11 (gfx950; gi_dense v11.3: dual steepest-edge select -s/|D[r,q:]| with a nonzero key floor, dependency scale clamped to FLT_MAX, setup slacks from the sweep's DPP-read f, output stores under the A-row loads, DPP-fused slack product and Householder update, Householder product as u + alpha D[:,q], exact ratio step, one-trip loads and x gather, 3 waves/SIMD; gi_box v2.1: lb <= x <= ub, A implicit, dual steepest-edge select with a nonzero key floor, DPP-fused slack and Householder products, one-pass R column shift; gi_wave v6.3: dual steepest-edge select with a nonzero key floor, ratio reduction only when a partial step is possible, active A rows for x gathered 16 at a time, DPP-fused sweep, slack product, Householder update and back substitution (no LDS vector reads), Householder product as u + alpha D[:,q], padded R, one-trip A gather for x, split setup sweep, 3 waves/SIMD; gi_gram v4.5 n<=128 on fp64 MFMA, no next-QP prefetch, lane ids opaque per iteration (2 VGPR spills instead of 29), active set as Q1 rows and Z = R^{-1} (parallel passes only), |u|^2 published with the key, broadcast row products, conflict-free diagonal-tile inverses, one-trip loads, cached workspace launched under its lock; ref v5: n <= 128, above 64 one LDS matrix per workgroup (LU, W / V, P in turn), LU rows staged for the solves, branch-free chunked sums)"; }
+extern "C" const char *qpb_version(void) { return "qpb 0.11 (gfx950; gi_dense v11.3: dual steepest-edge select -s/|D[r,q:]| with a nonzero key floor, dependency scale clamped to FLT_MAX, setup slacks from the sweep's DPP-read f, output stores under the A-row loads, DPP-fused slack product and Householder update, Householder product as u + alpha D[:,q], exact ratio step, one-trip loads and x gather, 3 waves/SIMD; gi_box v2.1: lb <= x <= ub, A implicit, dual steepest-edge select with a nonzero key floor, DPP-fused slack and Householder products, one-pass R column shift; gi_wave v6.4 (+ BOX, n <= 32): dual steepest-edge select with a nonzero key floor, ratio reduction only when a partial step is possible, active A rows for x gathered 16 at a time, DPP-fused sweep, slack product, Householder update and back substitution (no LDS vector reads), Householder product as u + alpha D[:,q], padded R, one-trip A gather for x, split setup sweep, 3 waves/SIMD; gi_gram v4.5 n<=128 on fp64 MFMA, no next-QP prefetch, lane ids opaque per iteration (2 VGPR spills instead of 29), active set as Q1 rows and Z = R^{-1} (parallel passes only), |u|^2 published with the key, broadcast row products, conflict-free diagonal-tile inverses, one-trip loads, cached workspace launched under its lock; ref v5: n <= 128, above 64 one LDS matrix per workgroup (LU, W / V, P in turn), LU rows staged for the solves, branch-free chunked sums)"; }

@@ -31,6 +31,14 @@
 //
 // LDS per QP (one wave): L packed rows (n(n+1)/2), R column-major NP x NP with
 // zero diagonal, the pivot / exchange vector, the y / x capture.
+//
+// BOX (round 5, qpb_solve_box for 16 < n <= 32): lb <= x <= ub with
+// A = [I; -I], b = [ub; -lb] kept implicit -- the constraint class of the
+// reference's admm() (qp_solvers.c:255-319, box config.h:29-30) at the
+// reference's larger N_DIM.  Row l of D starts from +-e (no A is read: 9.7 KB
+// per QP at n = 32 instead of 26.1 KB), the same sweep turns it into
+// +-row of L^{-T}, the loop is unchanged, and x = -H^{-1}(f + lam_u - lam_l)
+// needs no A rows.  Absent bounds (NULL or +-inf) have slack +inf.
 #include <type_traits>
 
 #include "qpb_common.h"
@@ -99,7 +107,7 @@ __device__ __forceinline__ void dpp_ready2(double a, double b) { asm volatile("s
 // REDO: solve only the QPs the mixed-precision kernel marked (status
 // kRedoStatus, qpb_gi_mixed.hip); every other wave exits at once
 constexpr int32_t kRedoStatus = 100;
-template <int OCC, bool STAMP = false, bool REDO = false>
+template <int OCC, bool STAMP = false, bool REDO = false, bool BOX = false>
 __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg, uint32_t *__restrict__ actg,
@@ -118,8 +126,9 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   double *xch = lds + OFF_X;
 
   const double *Hq = Hg + g * (long long)n * n;
-  const double *Aq = m > 0 ? Ag + g * (long long)m * n : Hq;
-  const double *bq = m > 0 ? bg + g * (long long)m : Hq;
+  // BOX: Ag = lb, bg = ub (n per QP, either may be NULL), m = 2n
+  const double *Aq = BOX ? Hq : m > 0 ? Ag + g * (long long)m * n : Hq;
+  const double *bq = BOX ? Hq : m > 0 ? bg + g * (long long)m : Hq;
   const bool rowok = l < m;
 
   // ------------------------------------------------------------------ load
@@ -132,7 +141,17 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // read back as half a row per lane (lane r: columns 0-15, lane r + 32:
   // columns 16-31, the sweep's split layout).
   double Lr[NH], E[NP];
-  const double bv = bq[rowok ? l : 0];
+  double bv;
+  if constexpr (BOX) {
+    // row l < n: x_l <= ub_l; row n + i: -x_i <= -lb_i (absent: +inf)
+    const int bi = l < n ? l : (l < 2 * n ? l - n : 0);
+    const double *bnd = l < n ? bg : Ag;
+    const double v = bnd ? bnd[g * n + bi] : kInf;
+    bv = l < n ? v : -v;
+    if (!(bv == bv)) bv = kInf;  // NaN bound: absent
+  } else {
+    bv = bq[rowok ? l : 0];
+  }
   const double fv = fg[g * n + (l < n ? l : 0)];
   {
     constexpr int RST = NP + 2;  // staged row stride
@@ -144,8 +163,10 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       // clamped, not masked: lane-vs-runtime compares would be hoisted into
       // SGPR masks; elements past the end land in rows nobody reads
       hv[i] = Hq[min(e, nn - 1)];
-      av[0][i] = Aq[max(min(e, h0 - 1), 0)];
-      av[1][i] = Aq[max(h0 + min(e, h1 - 1), 0)];
+      if constexpr (!BOX) {
+        av[0][i] = Aq[max(min(e, h0 - 1), 0)];
+        av[1][i] = Aq[max(h0 + min(e, h1 - 1), 0)];
+      }
     }
     // flat element e = i*64 + l -> (row, col) of an n-column matrix, stepped
     // per i by 64 = q0*n + r0 (n > 16, so one wrap per step at most)
@@ -184,17 +205,23 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       if (i * 128 + 2 * l < (NP + 1) * RST)
         *reinterpret_cast<double2 *>(&lds[i * 128 + 2 * l]) = make_double2(0.0, 0.0);
     wave_lds_sync();
-    // A first: the 64 loaded registers of A are released before L's 64 are
-    // filled (peak E + L + H's 32 staged values, not E + L + A)
-    stage(av[0]);
-    wave_lds_sync();
-    fetch_row(E, l & (NP - 1), l < NP && rowok);
-    wave_lds_sync();
-    if (m > NP) {
-      stage(av[1]);
+    if constexpr (BOX) {
+      // row l: +e_l (l < n), -e_{l-n} (n <= l < 2n)
+#pragma unroll
+      for (int j = 0; j < NP; ++j) E[j] = (l == j && l < n) ? 1.0 : (l - n == j && l < 2 * n) ? -1.0 : 0.0;
+    } else {
+      // A first: the 64 loaded registers of A are released before L's 64 are
+      // filled (peak E + L + H's 32 staged values, not E + L + A)
+      stage(av[0]);
       wave_lds_sync();
-      fetch_row(E, l & (NP - 1), l >= NP && rowok);
+      fetch_row(E, l & (NP - 1), l < NP && rowok);
       wave_lds_sync();
+      if (m > NP) {
+        stage(av[1]);
+        wave_lds_sync();
+        fetch_row(E, l & (NP - 1), l >= NP && rowok);
+        wave_lds_sync();
+      }
     }
     stage(hv);
     wave_lds_sync();
@@ -574,7 +601,17 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // L^T x = -y lane-parallel (L read from LDS, broadcasts by v_readlane)
   double gl = fl;
   const int ll = l & (NP - 1);
-  {
+  double *lamb = R;  // lambda by row (64 entries over xch + the start of R)
+  if constexpr (BOX) {
+    // a_k = +e_k (k < n) or -e_{k-n}: g_l = f_l + lam[l] - lam[n + l], the
+    // multipliers scattered by row first (no A rows to gather)
+    wave_lds_sync();
+    lamb[l] = 0.0;
+    wave_lds_sync();
+    if (l < q && iam >= 0) lamb[iam] = um;
+    wave_lds_sync();
+    if (l < n) gl = fl + (lamb[l] - lamb[n + l]);
+  } else {
     // every active row's element first (one memory round trip instead of q
     // dependent ones), 16 at a time (one trip for q <= 16, the usual case;
     // 8 at a time was 0.3-0.6 % slower), then the sum in position order
@@ -636,12 +673,13 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   }
   if (status == QPB_OK && wave_any(l < n && !(__builtin_fabs(xl) < kInf))) status = QPB_NUMERICAL;
   clk.tick(10);  // x = -H^{-1} (f + A^T lam)
-  // lambda scatter through LDS (64 entries over xch + the start of R)
-  wave_lds_sync();
-  double *lamb = R;
-  lamb[l] = 0.0;
-  wave_lds_sync();
-  if (l < q && iam >= 0) lamb[iam] = um;
+  // lambda scatter through LDS (64 entries over xch + the start of R; BOX: done above)
+  if constexpr (!BOX) {
+    wave_lds_sync();
+    lamb[l] = 0.0;
+    wave_lds_sync();
+    if (l < q && iam >= 0) lamb[iam] = um;
+  }
   wave_lds_sync();
   if (rowok) lamg[g * m + l] = lamb[l];
   if (l < n) xg[g * n + l] = xl;
@@ -694,5 +732,16 @@ extern "C" hipError_t qpb_launch_gi_wave_redo(const qpb_desc *d, const double *H
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
   hipLaunchKernelGGL((qpb::wv::gi_wave_kernel<2, false, true>), dim3((unsigned)d->batch), dim3(64), 0, stream, H, f,
                      A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol);
+  return hipGetLastError();
+}
+
+// qpb_solve_box for 16 < n <= 32 (m = 2n): A = [I; -I], b = [ub; -lb] implicit
+extern "C" hipError_t qpb_launch_gi_wave_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
+                                             const double *ub, double *x, double *lam, uint32_t *active,
+                                             int32_t *status, int32_t *iters, hipStream_t stream) {
+  const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
+  const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
+  hipLaunchKernelGGL((qpb::wv::gi_wave_kernel<3, false, false, true>), dim3((unsigned)d->batch), dim3(64), 0, stream,
+                     H, f, lb, ub, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol);
   return hipGetLastError();
 }

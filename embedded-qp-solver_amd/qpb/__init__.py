@@ -161,7 +161,7 @@ def solve(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0, out
 def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, feas_tol: float = 0.0, out: Solution | None = None,
               stream=None) -> Solution:
     """Batched min 1/2 x^T H x + f^T x s.t. lb <= x <= ub on the GPU (qpb_solve_box,
-    n <= 16): the reference admm()'s box QP (qp_solvers.c:146-319), solved exactly.
+    n <= 32): the reference admm()'s box QP (qp_solvers.c:146-319), solved exactly.
 
     H (B,n,n), f (B,n), lb / ub (B,n) CUDA float64 tensors or None (absent
     bounds; +-inf entries likewise).  The Solution has m = 2n: lam[:, :n] and
@@ -184,7 +184,7 @@ def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, feas_tol: float = 0.
     if out is None:
         out = Solution(torch.empty((B, n), dtype=torch.float64, device=dev),
                        torch.empty((B, m), dtype=torch.float64, device=dev),
-                       torch.empty((B, 1), dtype=torch.int32, device=dev),
+                       torch.empty((B, (m + 31) // 32), dtype=torch.int32, device=dev),
                        torch.empty((B,), dtype=torch.int32, device=dev),
                        torch.empty((B,), dtype=torch.int32, device=dev))
     d = Desc(n, m, B, max_iter, 0, feas_tol)

@@ -129,10 +129,11 @@ int qpb_solve_host(const qpb_desc *desc, const double *H, const double *f,
 
 /* Box-constrained batched solve, lb <= x <= ub: the constraint class of the
  * reference's admm() (qp_solvers.c:146-319, bounds config.h:29-30), solved
- * exactly with A = [I; -I], b = [ub; -lb] kept implicit (qpb_gi_box.hip).
- * Replaces admm()'s box QP the way qpb_solve replaces the dense path.
- * desc->n <= 16 (QPB_ERR_UNSUPPORTED above; pass the dense A = [I; -I] to
- * qpb_solve there); desc->m must be 2n.  lb, ub: B x n, either may be NULL,
+ * exactly with A = [I; -I], b = [ub; -lb] kept implicit (qpb_gi_box.hip for
+ * n <= 16, four QPs per wavefront; the BOX form of qpb_gi_wave.hip for
+ * 16 < n <= 32, one QP per wavefront).  Replaces admm()'s box QP the way
+ * qpb_solve replaces the dense path.  desc->n <= 32 (QPB_ERR_UNSUPPORTED
+ * above; pass the dense A = [I; -I] to qpb_solve there); desc->m must be 2n.  lb, ub: B x n, either may be NULL,
  * and +-inf entries are absent bounds.  lam: B x 2n (upper bounds' multipliers
  * first, then the lower bounds'), active: B words in the same row order;
  * x, status, iters as qpb_solve.  Device pointers; asynchronous on `stream`. */

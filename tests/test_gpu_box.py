@@ -1,4 +1,5 @@
-"""GPU parity of the box-constrained kernel (qpb_gi_box.hip, qpb_solve_box):
+"""GPU parity of the box-constrained kernels (qpb_solve_box: qpb_gi_box.hip for
+n <= 16, the BOX form of qpb_gi_wave.hip for 16 < n <= 32):
 lb <= x <= ub with A = [I; -I] kept implicit -- the constraint class of the
 reference's admm() (qp_solvers.c:146-319).  Oracles: the KKT-certified primal
 active set (oracle.active_set_solve) on the same QPs written with a dense
@@ -49,7 +50,7 @@ def _np(sol):
     return [t.cpu().numpy() for t in sol]
 
 
-@pytest.mark.parametrize("n,count", [(16, 64), (4, 40), (7, 33), (13, 17), (1, 9)])
+@pytest.mark.parametrize("n,count", [(16, 64), (4, 40), (7, 33), (13, 17), (1, 9), (20, 24), (32, 32), (25, 9)])
 def test_box_matches_oracle(qpb, n, count):
     H, f, lb, ub = _family(100 + n, count, n)
     x, lam, act, st, it = _np(qpb.solve_box(*_cuda(H, f, lb, ub)))
@@ -66,7 +67,7 @@ def test_box_matches_oracle(qpb, n, count):
         assert np.abs(lam[i] - ref.lam).max() / (1.0 + np.abs(ref.lam).max()) <= TOL, i
 
 
-@pytest.mark.parametrize("n", [16, 9])
+@pytest.mark.parametrize("n", [16, 9, 20, 32])
 def test_box_matches_dense_path(qpb, n):
     """The same QPs through qpb_solve with the dense A = [I; -I]: same active
     sets and statuses, x and lambda to rounding."""
@@ -82,8 +83,9 @@ def test_box_matches_dense_path(qpb, n):
     assert np.abs(ib.astype(int) - idd.astype(int)).max() <= 2  # selection ties may reorder steps
 
 
-def test_box_one_sided_and_absent_bounds(qpb):
-    n, B = 16, 200
+@pytest.mark.parametrize("n", [16, 32])
+def test_box_one_sided_and_absent_bounds(qpb, n):
+    B = 200
     H, f, lb, ub = _family(31, B, n)
     # no bounds at all: the unconstrained minimiser
     x, lam, act, st, _ = _np(qpb.solve_box(*_cuda(H, f, None, None)))
@@ -101,8 +103,8 @@ def test_box_one_sided_and_absent_bounds(qpb):
     assert np.array_equal(qpb.active_mask_to_bool(aa, 2 * n)[:, :n], qpb.active_mask_to_bool(ad, n))
 
 
-def test_box_statuses(qpb):
-    n = 16
+@pytest.mark.parametrize("n", [16, 32])
+def test_box_statuses(qpb, n):
     H, f, lb, ub = _family(5, 8, n)
     lb[3, 2] = ub[3, 2] + 1.0  # empty box -> INFEASIBLE
     H[5] = -H[5]  # not SPD
@@ -134,7 +136,7 @@ def test_box_metric_batch_kkt(qpb):
     assert max(float(v.max()) for v in r.values()) <= 1e-9
 
 
-@pytest.mark.parametrize("n", [16, 5])
+@pytest.mark.parametrize("n", [16, 5, 32, 24])
 def test_box_tiny_hessian_only_first_bound_violated(qpb, n):
     """ADVICE r03 on the box kernel: H = 1e-40 I and f scaled with it, only
     x_0's upper bound violated at the unconstrained minimiser.  The selection
@@ -154,3 +156,29 @@ def test_box_tiny_hessian_only_first_bound_violated(qpb, n):
     assert np.abs(x - x_ref).max() <= 1e-9
     mask = qpb.active_mask_to_bool(act, 2 * n)
     assert mask[:, 0].all() and mask.sum(axis=1).tolist() == [1] * B
+
+
+def test_box_config4_shape_batch(qpb):
+    """n = 32 (the configs[4] size class) at B = 262,144: the implicit-A box
+    kernel and the dense path on A = [I; -I] choose the same active set for
+    every QP, x to rounding, KKT on a sample of 2048 QPs."""
+    B, n = 262144, 32
+    H, f, A, b = qpb.generate(n, B, 20261015, family="box", device=torch.device("cuda", 0))
+    ub = b[:, :n].contiguous()
+    lb = (-b[:, n:]).contiguous()
+    sol = qpb.solve_box(H, f, lb, ub)
+    dense = qpb.solve(H, f, A, b)
+    torch.cuda.synchronize()
+    assert bool((sol.status == qpb.OK).all()) and bool((dense.status == qpb.OK).all())
+    assert torch.equal(sol.active, dense.active)
+    assert float((sol.x - dense.x).abs().max() / dense.x.abs().max().clamp(min=1.0)) <= 1e-10
+    idx = torch.arange(0, B, B // 2048, device=f.device)
+    Hs, fs, As, bs = (t[idx].cpu().numpy() for t in (H, f, A, b))
+    r = O.kkt_residuals(Hs, fs, As, bs, sol.x[idx].cpu().numpy(), sol.lam[idx].cpu().numpy())
+    assert max(float(v.max()) for v in r.values()) <= 1e-9
+
+
+def test_box_beyond_32_is_unsupported(qpb):
+    H, f, lb, ub = _family(3, 2, 33)
+    with pytest.raises(qpb.QPBError):
+        qpb.solve_box(*_cuda(H, f, lb, ub))
