@@ -50,7 +50,8 @@ def _np(sol):
     return [t.cpu().numpy() for t in sol]
 
 
-@pytest.mark.parametrize("n,count", [(16, 64), (4, 40), (7, 33), (13, 17), (1, 9), (20, 24), (32, 32), (25, 9)])
+@pytest.mark.parametrize("n,count", [(16, 64), (4, 40), (7, 33), (13, 17), (1, 9), (20, 24), (32, 32), (25, 9),
+                                     (17, 5), (31, 1)])
 def test_box_matches_oracle(qpb, n, count):
     H, f, lb, ub = _family(100 + n, count, n)
     x, lam, act, st, it = _np(qpb.solve_box(*_cuda(H, f, lb, ub)))

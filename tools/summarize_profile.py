@@ -51,6 +51,21 @@ for d in sorted(os.listdir(out_dir)) if os.path.isdir(out_dir) else []:
 if sq.get("SQ_WAVES"):
     res["sq_per_wave"] = {k: v / sq["SQ_WAVES"] for k, v in sq.items() if k != "SQ_WAVES"}
     res["sq_waves_per_launch"] = sq["SQ_WAVES"]
+# effective shader clock over the solver kernel: GRBM_GUI_ACTIVE sums the
+# busy cycles of the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back), so
+# cycles / 8 / the kernel's duration in the same pass
+clk = {}
+for r in rows(os.path.join(out_dir, "pmc_clk", "run_counter_collection.csv")):
+    if KERNEL in r["Kernel_Name"]:
+        clk.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+kt = rows(os.path.join(out_dir, "pmc_clk", "run_kernel_trace.csv"))
+durs = [float(r["End_Timestamp"]) - float(r["Start_Timestamp"]) for r in kt if KERNEL in r.get("Kernel_Name", "")]
+if clk.get("GRBM_GUI_ACTIVE") and durs:
+    ga = sum(clk["GRBM_GUI_ACTIVE"]) / len(clk["GRBM_GUI_ACTIVE"])
+    dn = sum(durs) / len(durs)
+    res["grbm_gui_active_per_launch"] = ga
+    res["pmc_pass_kernel_ns"] = dn
+    res["effective_clock_GHz"] = ga / 8.0 / dn
 try:
     res["bench"] = json.loads(open(os.path.join(out_dir, "bench.json")).read().strip().splitlines()[-1])
     res["library"] = res["bench"].get("library")
