@@ -100,7 +100,8 @@ def _digest_worker(rank, world, port, ret):
     dist.destroy_process_group()
 
 
-def test_gather_check_digests_catch_corruption_and_misplacement():
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_check_digests_catch_corruption_and_misplacement(world):
     """qpb.dist.check_gathered (bench.py --gather's check): every rank's exact
     integer digest of its shard against its rows of the batch gathered to rank
     0 -- equal for a correct gather, unequal for one flipped low bit in another
@@ -111,7 +112,7 @@ def test_gather_check_digests_catch_corruption_and_misplacement():
         port = s.getsockname()[1]
     mgr = mp.Manager()
     ret = mgr.dict()
-    mp.spawn(_digest_worker, args=(2, port, ret), nprocs=2, join=True)
-    assert ret["ok_0"] is True and ret["ok_1"] is True
-    assert ret["bad_0"] is False and ret["bad_1"] is True  # only rank 0 holds the batch
+    mp.spawn(_digest_worker, args=(world, port, ret), nprocs=world, join=True)
+    assert all(ret[f"ok_{r}"] is True for r in range(world))  # 11 QPs: uneven shards
+    assert ret["bad_0"] is False and all(ret[f"bad_{r}"] is True for r in range(1, world))  # only rank 0 holds the batch
     assert ret["swap_0"] is False
