@@ -358,8 +358,17 @@ __device__ __forceinline__ void gi_group(
   wave_lds_sync();
   clk.tick(3);
 
+#ifndef QPB_TAIL_PRIO
+#define QPB_TAIL_PRIO 0  // trip from which a wave raises its issue priority (0: never)
+#endif
   while (!done && it < max_iter) {
     ++it;
+#if QPB_TAIL_PRIO > 0
+    // a wave still running after QPB_TAIL_PRIO trips holds one of the long
+    // QPs that end a launch: it takes the VALU issue slots ahead of its
+    // SIMD partners (the tail)
+    if (it == QPB_TAIL_PRIO) __builtin_amdgcn_s_setprio(2);
+#endif
     if (selecting) {
       // The violation test is fp64 on the slack normalised by |a_row| (the
       // feasibility tolerance); among the violated rows the argmax runs on
