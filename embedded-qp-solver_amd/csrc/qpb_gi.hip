@@ -358,17 +358,8 @@ __device__ __forceinline__ void gi_group(
   wave_lds_sync();
   clk.tick(3);
 
-#ifndef QPB_TAIL_PRIO
-#define QPB_TAIL_PRIO 0  // trip from which a wave raises its issue priority (0: never)
-#endif
   while (!done && it < max_iter) {
     ++it;
-#if QPB_TAIL_PRIO > 0
-    // a wave still running after QPB_TAIL_PRIO trips holds one of the long
-    // QPs that end a launch: it takes the VALU issue slots ahead of its
-    // SIMD partners (the tail)
-    if (it == QPB_TAIL_PRIO) __builtin_amdgcn_s_setprio(2);
-#endif
     if (selecting) {
       // The violation test is fp64 on the slack normalised by |a_row| (the
       // feasibility tolerance); among the violated rows the argmax runs on
@@ -717,8 +708,28 @@ __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
     long long batch, int max_iter, double feas_tol, int flags = 0,
     unsigned long long *__restrict__ dbg = nullptr) {
   __shared__ double lds[QPB * SLOT];
+#ifdef QPB_WAVE_TRACE
+  // diagnostic build only (tools/wave_timeline.py): each wave's start and end
+  // on the 100 MHz real-time and the shader clocks, and where it ran
+  unsigned long long rt0, mt0, rt1, mt1;
+  unsigned hw, xcc;
+  asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0), "=s"(mt0)::"memory");
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+#endif
   gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
-                                 flags, dbg, blockIdx.x);
+                                 flags, STAMP ? dbg : nullptr, blockIdx.x);
+#ifdef QPB_WAVE_TRACE
+  asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1), "=s"(mt1)::"memory");
+  if (!STAMP && dbg && threadIdx.x == 0) {
+    unsigned long long *r = dbg + 8ull * blockIdx.x;
+    r[0] = rt0;
+    r[1] = rt1;
+    r[2] = mt0;
+    r[3] = mt1;
+    r[4] = hw | ((unsigned long long)xcc << 32);
+  }
+#endif
 }
 
 }  // namespace qpb
@@ -757,6 +768,16 @@ extern "C" hipError_t qpb_launch_gi_sections(const qpb_desc *d, const double *H,
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
   if (d->n != 16 || d->m <= 16) return hipErrorInvalidValue;
+#ifdef QPB_WAVE_TRACE
+  // the diagnostic build launches the shipped kernel and writes 8 words per
+  // wave: the caller's buffer holds 8 * ceil(batch / 4) (tools/wave_timeline.py)
+  if (d->m == 32) {
+    hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, true, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream,
+                       H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
+                       d->flags, sections);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL((qpb::gi_dense_kernel<2, true, false, true>), dim3((unsigned)blocks), dim3(64), 0, stream, H, f,
                      A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags,
                      sections);
