@@ -39,11 +39,13 @@
 // Data layout per QP (lane l = 0..15 of the QP's 16-lane DPP row):
 //   registers  rows l + 16 r (r < MR) of D, their slacks, 1/||a_row||,
 //              |D row|^2, |free part|^2, active flags; multiplier / row of
-//              active position l, R[l][l] and its reciprocal
-//   LDS        L (packed rows), R (16 x 16 column-major, zero diagonal),
-//              exchange row, Givens parameters, lambda scatter buffer.  The R
-//              area doubles as the staging buffer of the coalesced input
-//              transposes.
+//              active position l, R[l][l] and its reciprocal; in a DROP the
+//              parameters of Givens rotation l
+//   LDS        L (packed rows), R (16 x 16 column-major, zero diagonal; its
+//              column 0 carries the exchange row).  The whole slot is the staging buffer of the
+//              coalesced input transposes before the factorisation, and the
+//              dead R holds the lambda scatter and the x capture after the
+//              loop.
 // Every product with a vector held one entry per lane (d2, the Householder
 // vector) is a v_fmac_f64_dpp reading the entry from lane j by row_newbcast:
 // no LDS round trip, no copy of the vector in every lane.
@@ -64,17 +66,23 @@ constexpr int RS = 18;  // row stride (doubles) of the input transposes: conflic
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
 constexpr int L_SIZE = lrow(NL);  // 136
 
-// LDS slot of one QP: 426 doubles = 3,408 B, 13,632 B per wave -> 12 waves
-// per CU (3 per SIMD, matching the VGPR budget)
+// LDS slot of one QP: 394 doubles = 3,152 B, 12,608 B per wave -> 12 waves
+// per CU (3 per SIMD, matching the VGPR budget).  A CU holds 12 one-wave
+// workgroups of up to 12,800 B of LDS each and 11 from 13,056 B
+// (tools/probe/occupancy_probe.hip, measured on the MI355X): the round-4 slot
+// (426 doubles, 13,632 B per wave) ran 11 waves per CU, one SIMD in four
+// with two (the wave timeline, tools/wave_timeline.py).
 constexpr int OFF_L = 0;                  // L (136)
-constexpr int OFF_T = L_SIZE;             // R, column-major 16 x 16: R[i][j] at j*16 + i
-constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: exchange rows (MR x 16), s_p, |d|^2; Givens
-                                          // cos / sin (16 + 16); y / x capture; lambda scatter
-constexpr int SLOT = OFF_XCH + 34;        // 426 (4 x 426 x 8 B = 13,632 B per wave: 12 waves per CU)
+constexpr int OFF_T = L_SIZE;             // R, column-major 16 x 16: R[i][j] at j*16 + i;
+                                          // column 0 (no entry above the diagonal) doubles as
+                                          // the exchange row outside a DROP
+constexpr int OFF_XCH = OFF_T + NL * NL;  // 392: s_p, |d|^2 of the exchange
+constexpr int SLOT = OFF_XCH + 2;         // 394
+constexpr int kWaveLdsMax = 12800;        // bytes per one-wave workgroup for 12 per CU
 constexpr double kDepTol = 1e-24;         // |d2|^2 <= kDepTol |d|^2  <=>  z = 0
 static_assert(SLOT % 2 == 0 && OFF_T % 2 == 0 && OFF_XCH % 2 == 0, "b128 alignment");
-static_assert(4 * SLOT * 8 <= 160 * 1024 / 12, "12 waves (3 per SIMD) per CU by LDS");
-static_assert(NL * RS <= SLOT - OFF_T, "input transposes are staged in T + xch");
+static_assert(4 * SLOT * 8 <= kWaveLdsMax, "12 waves (3 per SIMD) per CU by LDS");
+static_assert(NL * RS <= SLOT, "input transposes are staged over the whole slot");
 
 // sum_{j<N} x(j) y(j) with 2 independent accumulators
 template <int N, class FX, class FY>
@@ -143,15 +151,16 @@ __device__ __forceinline__ void gi_group(
   }
 
   // LDS slots in the order 0, 2, 1, 3: ds_read_b64 serves 32 lanes (two QPs)
-  // per cycle, and SLOT = 424 doubles is 16 banks mod 64, so neighbouring
-  // slots would collide on contiguous 16-lane reads; slots 0/2 and 1/3 are
-  // 32 banks apart
+  // per cycle; slots 0/1 and 2/3 are 2 SLOT = 788 doubles apart, 40 banks mod
+  // 64, so contiguous 16-lane reads of the two QPs share 8 of the 64 banks
+  // (one slot apart they would share 20)
   double *base = lds + (((slot & 1) << 1) | (slot >> 1)) * SLOT;
   double *Lp = base + OFF_L;
   double *Tv = base + OFF_T;  // R, column-major (zero diagonal)
-  double *gcs = base + OFF_XCH;  // Givens cosines (DROP only)
-  double *gsn = gcs + NL;        // Givens sines
-  double *xch = base + OFF_XCH;
+  // the exchange row in R's column 0: the back substitution never reads that
+  // column, a DROP rebuilds it before use, an ADD at q = 0 rewrites it
+  double *xch = Tv;
+  double *xsd = base + OFF_XCH;  // s_p, |D[p,:]|^2
 
   // ------------------------------------------------------------------ load
   // (flags & QPB_FLAG_DIAG_L2: every QP reads the inputs of QP g mod 512;
@@ -176,11 +185,12 @@ __device__ __forceinline__ void gi_group(
   const double fv = fg[gi * n + (l < n ? l : n - 1)];
   const double fl = (N16 || l < n) ? fv : 0.0;
   [[maybe_unused]] const int hr = l >> 3, hc = 2 * (l & 7);
-  // stage 16 rows of a 16-column matrix (as loaded) in this QP's T region
+  // stage 16 rows of a 16-column matrix (as loaded) in this QP's slot (L and
+  // R are written after the factorisation)
   auto stage = [&](const double2 (&v)[8]) {
     wave_lds_sync();
 #pragma unroll
-    for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&Tv[(2 * t + hr) * RS + hc]) = v[t];
+    for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&base[(2 * t + hr) * RS + hc]) = v[t];
     wave_lds_sync();
   };
   // row r's constant data from its entries: the violation threshold of the
@@ -198,7 +208,7 @@ __device__ __forceinline__ void gi_group(
     // Coalesced 16-byte loads: one instruction reads 2 whole rows (256 B) of
     // each of the wave's 4 QPs -- lane l gets row 2t + (l>>3), columns
     // 2(l&7), 2(l&7)+1.  Rows reach their owner lane through a transpose in
-    // this QP's T region of LDS (free until the active-set loop).
+    // this QP's LDS slot (free until the factorisation ends).
     double2 hv[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) hv[t] = *reinterpret_cast<const double2 *>(&Hq[(2 * t + hr) * NL + hc]);
@@ -228,11 +238,11 @@ __device__ __forceinline__ void gi_group(
       for (int r = 0; r < MR; ++r) asm volatile("" ::"v"(av[r][t].x), "v"(av[r][t].y));
     }
     stage(hv);
-    lds_row16(&Tv[l * RS], Lr);
+    lds_row16(&base[l * RS], Lr);
 #pragma unroll
     for (int r = 0; r < MR; ++r) {
       stage(av[r]);
-      lds_row16(&Tv[l * RS], E[r]);
+      lds_row16(&base[l * RS], E[r]);
       row_norms(r, E[r]);
     }
     wave_lds_sync();
@@ -257,6 +267,13 @@ __device__ __forceinline__ void gi_group(
     }
   }
   clk.tick(0);
+#ifdef QPB_WAVE_TRACE
+  if (!STAMP && dbg) {  // diagnostic build: the inputs have arrived
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    if (threadIdx.x == 0) dbg[8ull * grp + 5] = t;
+  }
+#endif
 
   bool spd = true;
   double ya = fl;
@@ -404,12 +421,12 @@ __device__ __forceinline__ void gi_group(
         if (r == prow) {
 #pragma unroll
           for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[r][j], E[r][j + 1]);
-          *reinterpret_cast<double2 *>(&xch[NL]) = make_double2(s[r], (double)ddr[r]);
+          *reinterpret_cast<double2 *>(xsd) = make_double2(s[r], (double)ddr[r]);
         }
     }
     wave_lds_sync();
     const double Dpl = xch[l];
-    const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NL]);
+    const double2 spdd = *reinterpret_cast<const double2 *>(xsd);
     const double Dpq = xch[q & (NL - 1)];  // q == 16: an ADD is impossible (d2 = 0)
     const double sp = spdd.x, dd = spdd.y;  // s_p, |D[p,:]|^2
     wave_lds_sync();
@@ -431,7 +448,8 @@ __device__ __forceinline__ void gi_group(
       double nacc = (l < q) ? Dpl : 0.0;  // = -d1_l
       unroll<NL>([&](auto JJ) {
         constexpr int j = NL - 1 - JJ;
-        if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, Tv[j * NL + l]);
+        // (column 0 holds no entry above the diagonal: skipped)
+        if (j > 0 && j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, Tv[j * NL + l]);
       });
       rm = nacc * ninv;  // r_l (0 for l >= q)
     }
@@ -548,7 +566,9 @@ __device__ __forceinline__ void gi_group(
           for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&Tv[l * NL + j]) = make_double2(0.0, 0.0);
         }
       }
-      // Givens rotations restore the upper-triangular R
+      // Givens rotations restore the upper-triangular R; lane j keeps the
+      // parameters of rotation j, which the unrolled D update reads by DPP
+      double gc = 0.0, gs = 0.0;
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
         const double a = Tv[j * NL + j], bb = Tv[j * NL + j + 1];
@@ -560,15 +580,17 @@ __device__ __forceinline__ void gi_group(
           Tv[l * NL + j] = __builtin_fma(cj, rj, sj * rj1);
           Tv[l * NL + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
         }
-        gcs[j] = cj;  // same value from every lane
-        gsn[j] = sj;
+        if (l == j) {
+          gc = cj;
+          gs = sj;
+        }
       }
       wave_lds_sync();
       Tv[l * NL + q - 1] = 0.0;
       unroll<NL - 1>([&](auto JJ) {
         constexpr int j = JJ;
         if (j + 1 < qmax && j >= k && j < q - 1) {
-          const double cj = gcs[j], sj = gsn[j];
+          const double cj = bc<j>(gc), sj = bc<j>(gs);
 #pragma unroll
           for (int r = 0; r < MR; ++r) {
             const double e0 = E[r][j], e1 = E[r][j + 1];
@@ -605,6 +627,13 @@ __device__ __forceinline__ void gi_group(
   // ------------------------------------------------------------- outputs
   // (the active rows of A re-read, one coalesced 128-B row per active position)
   const int qm = __builtin_elementwise_min(wave_max4(q), NL);
+  // The QP index and its A block again, recomputed from an opaque copy of the
+  // slot instead of held across the loop (held, the allocator spilled them)
+  int slot_o = slot;
+  asm volatile("" : "+v"(slot_o));
+  const long long go = live ? grp * QPB + slot_o : batch - 1;
+  const long long gio = (flags & QPB_FLAG_DIAG_L2) ? (go & 511) : (flags & QPB_FLAG_DIAG_MALL) ? (go & 16383) : go;
+  const double *Aqo = m > 0 ? Ag + gio * (long long)m * n : Hg + gio * (long long)n * n;
   // The A-row loads go out first, in at most two groups of eight (one
   // wave-uniform test per group: a test per load made each load a branch
   // with its own wait); the work that does not need them -- the multipliers by
@@ -620,11 +649,12 @@ __device__ __forceinline__ void gi_group(
       __builtin_amdgcn_sched_barrier(0);
       unroll<8>([&](auto K) {
         constexpr int kk = k0 + K;
-        arow[kk] = Aq[bci<kk>(ias) * n + lc];
+        arow[kk] = Aqo[bci<kk>(ias) * n + lc];
       });
     }
   });
-  double *lamb = xch;  // lambda scatter (32); the solves below reuse xch afterwards
+  double *lamb = Tv;  // lambda scatter (32) over the dead R; the solves below capture in Tv[32:48]
+  double *xcap = Tv + 2 * NL;
 #pragma unroll
   for (int r = 0; r < 2; ++r) lamb[l + NL * r] = 0.0;
   wave_lds_sync();
@@ -641,7 +671,7 @@ __device__ __forceinline__ void gi_group(
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
     const int row = l + NL * r;
-    if (live && (FULL || row < m)) lamg[g * m + row] = lamr[r];
+    if (live && (FULL || row < m)) lamg[go * m + row] = lamr[r];
   }
   uint32_t w0 = 0;
 #pragma unroll
@@ -649,7 +679,7 @@ __device__ __forceinline__ void gi_group(
     const unsigned long long bal = __ballot(act[r]);
     w0 |= (uint32_t)((bal >> sh) & 0xFFFFull) << (16 * r);
   }
-  if (live && l == 0 && m > 0) actg[g] = w0;
+  if (live && l == 0 && m > 0) actg[go] = w0;
   // x = -H^{-1} (f + A^T lam): g = f + sum_k u_k a_{iam_k}, then L y = g,
   // L^T x = -y, lane-parallel: step k broadcasts the finished component from
   // lane k; finished lanes keep updating (dead values) and the components are
@@ -670,31 +700,31 @@ __device__ __forceinline__ void gi_group(
       constexpr int kk = K;
       const double yk = bc<kk>(acc * invd);
       acc = __builtin_fma(-Lrow[kk], yk, acc);
-      xch[kk] = yk;
+      xcap[kk] = yk;
     });
   }
   wave_lds_sync();
   {
-    double acc = xch[l];
+    double acc = xcap[l];
     wave_lds_sync();
     unroll<NL>([&](auto K) {
       constexpr int kk = NL - 1 - K;
       const double xk = bc<kk>(acc * invd);
       acc = __builtin_fma(-Lp[lrow(kk) + l], xk, acc);
-      xch[kk] = xk;
+      xcap[kk] = xk;
     });
   }
   wave_lds_sync();
-  const double xl = -xch[l];
+  const double xl = -xcap[l];
   {
     // a non-finite x on any lane -> NUMERICAL for the QP
     const double bad = row_min((__builtin_fabs(xl) < kInf) ? 0.0 : -1.0);
     if (status == QPB_OK && bad < 0.0) status = QPB_NUMERICAL;
   }
-  if (live && (N16 || l < n)) xg[g * n + l] = xl;
+  if (live && (N16 || l < n)) xg[go * n + l] = xl;
   if (live && l == 0) {
-    statg[g] = status;
-    if (itg) itg[g] = it;
+    statg[go] = status;
+    if (itg) itg[go] = it;
   }
   clk.tick(11);
   clk.flush(dbg);
@@ -718,8 +748,15 @@ __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
 #endif
   gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
-                                 flags, STAMP ? dbg : nullptr, blockIdx.x);
 #ifdef QPB_WAVE_TRACE
+                                 flags, dbg, blockIdx.x);
+#else
+                                 flags, STAMP ? dbg : nullptr, blockIdx.x);
+#endif
+#ifdef QPB_WAVE_TRACE
+#if QPB_WAVE_TRACE == 2
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the end after the output stores have drained
+#endif
   asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1), "=s"(mt1)::"memory");
   if (!STAMP && dbg && threadIdx.x == 0) {
     unsigned long long *r = dbg + 8ull * blockIdx.x;

@@ -35,9 +35,13 @@ constexpr int L_SIZE = lrow(NL);  // 136
 constexpr int OFF_L = 0;
 constexpr int OFF_R = L_SIZE;
 constexpr int OFF_XCH = OFF_R + NL * NL;
-constexpr int SLOT = OFF_XCH + 32;  // 424 doubles
+constexpr int SLOT = OFF_XCH + 2;  // 394 doubles: s_p (the exchange row is R's column 0, as qpb_gi.hip)
 constexpr double kDepTol = 1e-24;
-static_assert(NL * RS <= SLOT - OFF_R, "the H transpose is staged in R + xch");
+static_assert(NL * RS <= SLOT, "the H transpose is staged over the whole slot");
+// 12 one-wave workgroups per CU need <= 12,800 B of LDS each (qpb_gi.hip,
+// tools/probe/occupancy_probe.hip); the round-4 slot (424 doubles = 13,568 B)
+// ran 11
+static_assert(4 * SLOT * 8 <= 12800, "12 waves per CU by LDS");
 
 template <int N, class FX, class FY>
 __device__ __forceinline__ double dot2(FX &&x, FY &&y) {
@@ -80,9 +84,8 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
   double *base = lds + (((slot & 1) << 1) | (slot >> 1)) * SLOT;  // slots 0, 2, 1, 3 (bank spread)
   double *Lp = base + OFF_L;
   double *R = base + OFF_R;
-  double *xch = base + OFF_XCH;
-  double *gcs = xch;       // Givens cosines (DROP only)
-  double *gsn = xch + NL;  // Givens sines
+  double *xch = R;  // the exchange row in R's column 0 (never read by the back substitution)
+  double *xsp = base + OFF_XCH;
 
   // ------------------------------------------------------------------ load
   const bool var = N16 || l < n;  // lane l carries variable l
@@ -95,7 +98,8 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
   double E[NL];   // row l of D = L^{-T}, from e_l
   if constexpr (N16) {
     // one instruction reads two whole rows of each of the wave's 4 QPs; the
-    // rows reach their owner lanes through a transpose in this QP's R region
+    // rows reach their owner lanes through a transpose in this QP's LDS slot
+    // (L and R are written after the factorisation)
     const int hr = l >> 3, hc = 2 * (l & 7);
     double2 hv[8];
 #pragma unroll
@@ -105,9 +109,9 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
     for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(hv[t].x), "v"(hv[t].y));
     wave_lds_sync();
 #pragma unroll
-    for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&R[(2 * t + hr) * RS + hc]) = hv[t];
+    for (int t = 0; t < 8; ++t) *reinterpret_cast<double2 *>(&base[(2 * t + hr) * RS + hc]) = hv[t];
     wave_lds_sync();
-    lds_row16(&R[l * RS], Lr);
+    lds_row16(&base[l * RS], Lr);
     wave_lds_sync();
   } else {
 #pragma unroll
@@ -212,12 +216,12 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
     if (l == owner) {
 #pragma unroll
       for (int j = 0; j < NL; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[j], E[j + 1]);
-      xch[NL] = p < NL ? su : sl;
+      *xsp = p < NL ? su : sl;
     }
     wave_lds_sync();
     const double wl = xch[l];
-    const double wq = xch[q];  // q == 16 reads s_p: only used by an ADD, impossible then
-    const double sp = xch[NL];
+    const double wq = xch[q & (NL - 1)];  // q == 16: only used by an ADD, impossible then
+    const double sp = *xsp;
     // the selected row with its active columns zeroed, entry j at lane j
     // (d2 = sgn * w2): the products below take it by DPP broadcast
     const double w2 = l >= q ? wl : 0.0;
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
       double nacc = (l < q) ? Dpl : 0.0;
       unroll<NL>([&](auto JJ) {
         constexpr int j = NL - 1 - JJ;
-        if (j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, R[j * NL + l]);
+        if (j > 0 && j < qmax) fmac_bc_nop<j>(nacc, nacc * ninv, R[j * NL + l]);  // column 0: no entry above the diagonal
       });
       rm = nacc * ninv;
     }
@@ -344,7 +348,9 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
             *reinterpret_cast<double2 *>(&R[l * NL + ((2 * t + 2 * l) & (NL - 1))]) = make_double2(0.0, 0.0);
         }
       }
-      // Givens rotations restore the upper-triangular R ...
+      // Givens rotations restore the upper-triangular R (lane j keeps rotation
+      // j's parameters for the D update, which reads them by DPP) ...
+      double gc = 0.0, gs = 0.0;
       for (int j = k; j < q - 1; ++j) {
         wave_lds_sync();
         const double a = R[j * NL + j], bb = R[j * NL + j + 1];
@@ -356,8 +362,10 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
           R[l * NL + j] = __builtin_fma(cj, rj, sj * rj1);
           R[l * NL + j + 1] = (l == j) ? 0.0 : __builtin_fma(-sj, rj, cj * rj1);
         }
-        gcs[j] = cj;  // same value from every lane
-        gsn[j] = sj;
+        if (l == j) {
+          gc = cj;
+          gs = sj;
+        }
       }
       wave_lds_sync();
       R[l * NL + q - 1] = 0.0;
@@ -365,7 +373,7 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
       unroll<NL - 1>([&](auto JJ) {
         constexpr int j = JJ;
         if (j + 1 < qmax && j >= k && j < q - 1) {
-          const double cj = gcs[j], sj = gsn[j];
+          const double cj = bc<j>(gc), sj = bc<j>(gs);
           const double e0 = E[j], e1 = E[j + 1];
           E[j] = __builtin_fma(cj, e0, sj * e1);
           E[j + 1] = __builtin_fma(-sj, e0, cj * e1);
@@ -395,7 +403,8 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
 
   // ------------------------------------------------------------- outputs
   // multipliers by constraint (row l: upper bound of x_l, row 16 + l: lower)
-  double *lamb = xch;
+  double *lamb = R;  // 32 over the dead R; the solves capture in R[32:48]
+  double *xcap = R + 2 * NL;
   wave_lds_sync();
   lamb[l] = 0.0;
   lamb[l + NL] = 0.0;
@@ -417,22 +426,22 @@ __global__ __launch_bounds__(64, 3) void gi_box_kernel(const double *__restrict_
       constexpr int kk = K;
       const double yk = bc<kk>(acc * invd);
       acc = __builtin_fma(-Lrow[kk], yk, acc);
-      xch[kk] = yk;
+      xcap[kk] = yk;
     });
   }
   wave_lds_sync();
   {
-    double acc = xch[l];
+    double acc = xcap[l];
     wave_lds_sync();
     unroll<NL>([&](auto K) {
       constexpr int kk = NL - 1 - K;
       const double xk = bc<kk>(acc * invd);
       acc = __builtin_fma(-Lp[lrow(kk) + l], xk, acc);
-      xch[kk] = xk;
+      xcap[kk] = xk;
     });
   }
   wave_lds_sync();
-  const double xl = -xch[l];
+  const double xl = -xcap[l];
   {
     const double bad = row_min((__builtin_fabs(xl) < kInf) ? 0.0 : -1.0);
     if (status == QPB_OK && bad < 0.0) status = QPB_NUMERICAL;

@@ -2,7 +2,8 @@
 """A/B timing of libqpb variants (tools/build_variant.sh) on the same batch,
 rounds interleaved so clock/thermal drift hits every variant alike.
   python tools/ab.py name1 name2 ...   ('head' = lib/libqpb.so; name@flags adds qpb_desc.flags)
-env: B (1048576), FAM (box), ROUNDS (5), REPS (6), MAXIT (0 = the default cap; 1 = setup + one trip)"""
+env: B (1048576), FAM (box), ROUNDS (5), REPS (6), MAXIT (0 = the default cap; 1 = setup + one trip),
+     BOXAPI (1: time qpb_solve_box on the same QPs, lb = -b[n:], ub = b[:n])"""
 import ctypes
 import json
 import os
@@ -22,7 +23,9 @@ def main(names):
     fam = os.environ.get("FAM", "box")
     rounds, reps = int(os.environ.get("ROUNDS", 5)), int(os.environ.get("REPS", 6))
     maxit = int(os.environ.get("MAXIT", 0))
+    boxapi = os.environ.get("BOXAPI", "0") == "1"
     H, f, A, b = qpb.generate(16, B, 1, family=fam, shift=1.0, box=10.0, device=dev)
+    ub, lb = b[:, :16].contiguous(), (-b[:, 16:]).contiguous()
     libs, fl = {}, {}
     for nm in names:
         base, _, fs = nm.partition("@")  # name@flags: the same library with qpb_desc.flags
@@ -30,15 +33,17 @@ def main(names):
         path = os.path.join(ROOT, "embedded-qp-solver_amd", "lib", f"libqpb_{base}.so" if base else "libqpb.so")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         lib.qpb_solve.argtypes = [ctypes.POINTER(qpb.Desc)] + [ctypes.c_void_p] * 10
+        lib.qpb_solve_box.argtypes = [ctypes.POINTER(qpb.Desc)] + [ctypes.c_void_p] * 10
         libs[nm] = lib
     s = torch.cuda.current_stream()
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    sols = {nm: qpb.solve(H, f, A, b) for nm in names}
+    sols = {nm: (qpb.solve_box(H, f, lb, ub) if boxapi else qpb.solve(H, f, A, b)) for nm in names}
     def call(nm):
         o = sols[nm]
         d = qpb.Desc(16, 32, B, maxit, fl[nm], 0.0)
-        rc = libs[nm].qpb_solve(ctypes.byref(d), p(H), p(f), p(A), p(b), p(o.x), p(o.lam), p(o.active), p(o.status),
-                                p(o.iters), ctypes.c_void_p(s.cuda_stream))
+        fn, a3, a4 = (libs[nm].qpb_solve_box, lb, ub) if boxapi else (libs[nm].qpb_solve, A, b)
+        rc = fn(ctypes.byref(d), p(H), p(f), p(a3), p(a4), p(o.x), p(o.lam), p(o.active), p(o.status),
+                p(o.iters), ctypes.c_void_p(s.cuda_stream))
         assert rc == 0, rc
 
     times = {nm: [] for nm in names}
@@ -62,7 +67,8 @@ def main(names):
         same = bool(torch.equal(sols[nm].x, sols[ref].x) and torch.equal(sols[nm].active, sols[ref].active))
         out[nm or "head"] = {"median_us": round(t[len(t) // 2], 1), "min_us": round(t[0], 1),
                              "same_as_first": same, "iters_mean": float(sols[nm].iters.double().mean())}
-    print(json.dumps({"B": B, "family": fam, "max_iter": maxit, "variants": out}, indent=1))
+    print(json.dumps({"B": B, "family": fam, "max_iter": maxit, "api": "qpb_solve_box" if boxapi else "qpb_solve",
+                      "variants": out}, indent=1))
 
 
 if __name__ == "__main__":

@@ -79,6 +79,7 @@ assert (r[:, 1] > 0).all(), "every wave wrote its record"
 
 rt0 = r[:, 0].astype(np.int64)
 rt1 = r[:, 1].astype(np.int64)
+rtl = r[:, 5].astype(np.int64)  # the inputs have arrived
 mt = (r[:, 3] - r[:, 2]).astype(np.float64)
 hw = (r[:, 4] & np.uint64(0xFFFFFFFF)).astype(np.int64)
 xcc = (r[:, 4] >> np.uint64(32)).astype(np.int64) & 0xF
@@ -128,6 +129,31 @@ for k, idx in enumerate(starts_by):
     for i in range(OCC, len(ss)):
         gaps.append(ss[i] - ends_sorted[i - OCC])
 gaps = np.array(gaps)
+
+
+def concurrency(key):
+    """time share of each resident-wave count over the units `key` names
+    (CUs, SIMDs), and each unit's maximum"""
+    ks, iv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    share = {}
+    mx = []
+    for idx in np.split(np.lexsort((s, iv)), np.cumsum(cnt)[:-1]):
+        ev_t = np.concatenate([s[idx], e[idx]])
+        ev_d = np.concatenate([np.ones(len(idx)), -np.ones(len(idx))])
+        o = np.lexsort((ev_d, ev_t))
+        ev_t, ev_d = ev_t[o], ev_d[o]
+        c = np.cumsum(ev_d).astype(int)
+        dt = np.diff(np.concatenate([ev_t, [span]]))
+        for ci in np.unique(c):
+            share[int(ci)] = share.get(int(ci), 0.0) + float(dt[c == ci].sum())
+        mx.append(int(c.max()))
+    tot_t = len(ks) * span
+    return ({str(k): round(v / tot_t, 4) for k, v in sorted(share.items())},
+            {str(v): int(n) for v, n in zip(*np.unique(mx, return_counts=True))})
+
+
+cu_share, cu_max = concurrency(simd_key >> 2)
+simd_share, simd_max = concurrency(simd_key)
 tot = nsimd * span
 clock = mt / ((rt1 - rt0) * 10e-9) / 1e9  # GHz
 resident = life.sum() / (OCC * nsimd * span)
@@ -146,8 +172,14 @@ out = {
     "span_us": float(span),
     "wave_lifetime_us": {"mean": float(life.mean()), "p50": float(np.median(life)),
                          "p99": float(np.percentile(life, 99)), "max": float(life.max())},
+    "input_wait_us": {"mean": float(((rtl - rt0) * 0.01).mean()), "p50": float(np.median((rtl - rt0) * 0.01)),
+                      "p90": float(np.percentile((rtl - rt0) * 0.01, 90))},
+    "end_after_store_drain": "wtrace2" in qpb.LIB_PATH,
     "slot_fill": float(resident),
     "time_share_by_resident_waves": {str(k): round(v / tot, 4) for k, v in fill.items()},
+    "cu_time_share_by_resident_waves": cu_share,
+    "cu_max_resident_waves": cu_max,
+    "simd_max_resident_waves": simd_max,
     "steady_state_share_below_occ": round(short_steady / max(1e-9, sum(fill_steady.values())), 4),
     "ramp_us_mean": float(ramp_t.mean()),
     "tail_us": {"mean": float(tail_t.mean()), "max": float(tail_t.max()), "min": float(tail_t.min())},
@@ -167,6 +199,7 @@ for lo, hi in zip(s, e):
 out["resident_waves_per_10us_bin"] = occ.astype(int).tolist()
 od = os.path.join(ROOT, "gpurun_out", "wtrace")
 os.makedirs(od, exist_ok=True)
-with open(os.path.join(od, f"wave_timeline_{fam}_{B}.json"), "w") as fh:
+tag = "_drain" if "wtrace2" in qpb.LIB_PATH else ""
+with open(os.path.join(od, f"wave_timeline_{fam}_{B}{tag}.json"), "w") as fh:
     json.dump(out, fh, indent=1)
 print(json.dumps({k: v for k, v in out.items() if k not in ("resident_waves_per_10us_bin", "library")}, indent=1))
