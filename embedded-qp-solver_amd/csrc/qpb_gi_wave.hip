@@ -53,12 +53,17 @@ constexpr int NP = 32;                              // padded n
 constexpr int NH = NP / 2;                          // H / L row half held per lane
 constexpr int L_SIZE = NP * (NP + 1) / 2;           // 528
 constexpr int OFF_L = 0;
-constexpr int RS = NP + 2;                          // R column stride: row-wise reads and writes
-                                                    // (DROP's Givens, the column shift) stay
-                                                    // conflict-free, columns 16-byte aligned
-constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*RS + i
-constexpr int OFF_X = OFF_R + NP * RS;              // 1616: exchange row (NP) + s_p, |d|^2; pivots
-constexpr int SLOT = OFF_X + NP + 8;                // 1656 doubles = 13,248 B (12 waves per CU)
+constexpr int RS = NP + 1;                          // R column stride (odd): row-wise and column-
+                                                    // wise b64 accesses both conflict-free
+constexpr int OFF_R = L_SIZE;                       // 528: R[i][j] at j*RS + i; column 0 (no entry
+                                                    // above the diagonal) doubles as the exchange row
+constexpr int OFF_X = OFF_R + NP * RS;              // 1584: s_p, |d|^2 of the exchange
+constexpr int SLOT = OFF_X + 2;                     // 1586 doubles = 12,688 B
+// a CU holds 12 one-wave workgroups of <= 12,800 B of LDS (11 from 13,056 B:
+// tools/probe/occupancy_probe.hip); the round-4 slot (RS = 34, a separate
+// exchange row: 13,248 B) ran 11
+static_assert(SLOT * 8 <= 12800, "12 waves (3 per SIMD) per CU by LDS");
+static_assert(OFF_R % 2 == 0 && OFF_X % 2 == 0, "b128 alignment of the exchange row and s_p");
 constexpr double kDepTol = 1e-24;
 
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
@@ -123,7 +128,8 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   }
   double *Lp = lds + OFF_L;
   double *R = lds + OFF_R;
-  double *xch = lds + OFF_X;
+  double *xch = R;             // the exchange row: R's column 0, never read by the back substitution
+  double *xsd = lds + OFF_X;   // s_p, |D[p,:]|^2
 
   const double *Hq = Hg + g * (long long)n * n;
   // BOX: Ag = lb, bg = ub (n per QP, either may be NULL), m = 2n
@@ -382,14 +388,14 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
     if (l == p) {
 #pragma unroll
       for (int j = 0; j < NP; j += 2) *reinterpret_cast<double2 *>(&xch[j]) = make_double2(E[j], E[j + 1]);
-      *reinterpret_cast<double2 *>(&xch[NP]) = make_double2(s, dn);
+      *reinterpret_cast<double2 *>(xsd) = make_double2(s, dn);
     }
     wave_lds_sync();
     // row p as the DPP operand pair (entry j at lane j & 15 of every row),
     // d2 = its columns >= q
     const double XA = xch[li], XB = xch[NH + li];
     const double Dpq = xch[q < NP ? q : 0];
-    const double2 spdd = *reinterpret_cast<const double2 *>(&xch[NP]);
+    const double2 spdd = *reinterpret_cast<const double2 *>(xsd);
     const double sp = spdd.x, dd = spdd.y;
     const double Dpl = (l & NH) ? XB : XA;  // D[p][l], lanes 0-31
     const double d2A = li >= q ? XA : 0.0, d2B = li + NH >= q ? XB : 0.0;
@@ -413,7 +419,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
           double ra[4], rb[4];
           unroll<4>([&](auto I) {
             constexpr int j = j0 + 3 - I;
-            ra[I] = R[j * RS + li];
+            if constexpr (j > 0) ra[I] = R[j * RS + li];
             if constexpr (j >= NH) rb[I] = R[j * RS + NH + li];
           });
           unroll<4>([&](auto I) {
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
               const double tj = nB * ninvB;
               fmac_bc_nop<j - NH>(nA, tj, ra[I]);
               fmac_bc<j - NH>(nB, tj, rb[I]);
-            } else {
+            } else if constexpr (j > 0) {  // column 0: no entry above the diagonal
               const double tj = nA * ninvA;
               fmac_bc_nop<j>(nA, tj, ra[I]);
             }
@@ -531,21 +537,18 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
       wave_lds_sync();
       if (l < q) R[l * RS + l] = rdg;
       // columns k+1 .. q-1 move left by one, column q-1 clears: lane l copies
-      // column l+1 whole (rows >= q are zero), half a column per pass (DS
-      // instructions run in order, so each read precedes every lane's write)
+      // column l+1 whole (rows >= q are zero), a quarter column per pass (DS
+      // instructions run in order, so each read precedes every lane's write;
+      // b64: the odd stride leaves odd columns 8-byte aligned)
       const bool shift = l >= k && l < q - 1, clear = l == q - 1;
-      unroll<2>([&](auto Hh) {
-        constexpr int i0 = NH * Hh;
-        double2 col[NH / 2];
+      unroll<4>([&](auto Hh) {
+        constexpr int i0 = (NP / 4) * Hh;
+        double col[NP / 4];
         wave_lds_sync();
-        unroll<NH / 2>([&](auto I) {
-          col[I] = *reinterpret_cast<const double2 *>(&R[((lc + 1) & (NP - 1)) * RS + i0 + 2 * I]);
-        });
+        unroll<NP / 4>([&](auto I) { col[I] = R[((lc + 1) & (NP - 1)) * RS + i0 + I]; });
         wave_lds_sync();
         if (shift || clear) {
-          unroll<NH / 2>([&](auto I) {
-            *reinterpret_cast<double2 *>(&R[lc * RS + i0 + 2 * I]) = clear ? make_double2(0.0, 0.0) : col[I];
-          });
+          unroll<NP / 4>([&](auto I) { R[lc * RS + i0 + I] = clear ? 0.0 : col[I]; });
         }
       });
       for (int j = k; j < q - 1; ++j) {
@@ -601,7 +604,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   // L^T x = -y lane-parallel (L read from LDS, broadcasts by v_readlane)
   double gl = fl;
   const int ll = l & (NP - 1);
-  double *lamb = R;  // lambda by row (64 entries over xch + the start of R)
+  double *lamb = R;  // lambda by row (64 entries over the dead R)
   if constexpr (BOX) {
     // a_k = +e_k (k < n) or -e_{k-n}: g_l = f_l + lam[l] - lam[n + l], the
     // multipliers scattered by row first (no A rows to gather)
@@ -673,7 +676,7 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   }
   if (status == QPB_OK && wave_any(l < n && !(__builtin_fabs(xl) < kInf))) status = QPB_NUMERICAL;
   clk.tick(10);  // x = -H^{-1} (f + A^T lam)
-  // lambda scatter through LDS (64 entries over xch + the start of R; BOX: done above)
+  // lambda scatter through LDS (64 entries over the dead R; BOX: done above)
   if constexpr (!BOX) {
     wave_lds_sync();
     lamb[l] = 0.0;

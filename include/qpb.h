@@ -54,7 +54,7 @@ extern "C" {
 
 /* qpb_version() reports "qpb MAJOR.MINOR (...)" */
 #define QPB_VERSION_MAJOR 0
-#define QPB_VERSION_MINOR 11
+#define QPB_VERSION_MINOR 12
 
 /* limits of this build's kernels: n <= 16, m <= 32 one QP per 16-lane DPP
  * row (qpb_gi.hip); n <= 32, m <= 64 one QP per wavefront (qpb_gi_wave.hip);
