@@ -35,6 +35,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -112,7 +113,11 @@ def shard_time_prediction(n: int, m: int, family: str, shard_qps: int, total_qps
     if (n, m, family) != (16, 32, "box") or not os.path.exists(path):
         return None
     scan = json.load(open(path))
-    pts = sorted((int(k[1:-3]), v) for k, v in scan.items() if k.startswith("B") and k.endswith("_us"))
+    # back-to-back launch times where the scan has them (bench.py's timed
+    # steps are queued without a wait), else the waited-for single launches
+    kind = "_b2b_us" if any(k.endswith("_b2b_us") for k in scan) else "_us"
+    pts = sorted((int(m_.group(1)), v) for k, v in scan.items()
+                 for m_ in [re.match(r"^B(\d+)" + kind + "$", k)] if m_)
 
     def t_us(b):
         for (b0, t0), (b1, t1) in zip(pts, pts[1:]):
@@ -123,7 +128,9 @@ def shard_time_prediction(n: int, m: int, family: str, shard_qps: int, total_qps
     if ts is None or tt is None:
         return None
     return {"shard_kernel_ms": ts * 1e-3, "total_kernel_ms": tt * 1e-3, "kernel_bound_speedup": tt / ts,
-            "source": "profiles/batch_scan.json (one GPU, kernel time vs batch)", "revision": scan.get("revision")}
+            "source": "profiles/batch_scan.json (one GPU, kernel time vs batch, "
+                      + ("launches back to back)" if kind == "_b2b_us" else "single launches)"),
+            "revision": scan.get("revision")}
 
 
 def valu_ceiling(traffic, waves: int, kern_ms: float):

@@ -190,6 +190,11 @@ out = {
     "shader_clock_GHz": {"p10": float(np.percentile(clock, 10)), "p50": float(np.median(clock)),
                          "p90": float(np.percentile(clock, 90))},
 }
+# the shader clock the waves ran at, by their start time (100 us bins): does
+# the chip raise its clock during a launch?
+cb = (s // 100).astype(int)
+out["shader_clock_GHz_by_start_100us"] = [round(float(np.median(clock[cb == i])), 3) if (cb == i).any() else None
+                                          for i in range(int(cb.max()) + 1)]
 # chip-level resident waves in 10 us bins (the shape of ramp and tail)
 bins = np.arange(0.0, span + 10.0, 10.0)
 occ = np.zeros(len(bins) - 1)
