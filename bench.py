@@ -104,15 +104,19 @@ VALU_COST = {"FMA_F64": 5.24, "MUL_F64": 5.47, "ADD_F64": 5.47, "TRANS_F64": 17.
 SIMDS, CLOCK_GHZ = 1024, 2.4  # MI355X: 256 CUs x 4 SIMDs, peak engine clock
 
 
-def shard_time_prediction(n: int, m: int, family: str, shard_qps: int, total_qps: int):
+def shard_time_prediction(n: int, m: int, family: str, shard_qps: int, total_qps: int, library: str = ""):
     """One-GPU kernel time of a `shard_qps` launch and of the whole batch, by
     linear interpolation of the committed batch scan (profiles/batch_scan.json,
     tools/batch_scan.py, box family at n = 16, m = 32), and the speed-up the
-    kernel alone allows: T(total) / T(shard).  None outside the scanned range."""
+    kernel alone allows: T(total) / T(shard).  None outside the scanned range,
+    and None when the scan was taken on another revision of the hot kernel
+    than the loaded library's (its `revision` not among kernel_revisions)."""
     path = os.path.join(ROOT, "profiles", "batch_scan.json")
     if (n, m, family) != (16, 32, "box") or not os.path.exists(path):
         return None
     scan = json.load(open(path))
+    if library and scan.get("revision") not in kernel_revisions(library):
+        return None
     # back-to-back launch times where the scan has them (bench.py's timed
     # steps are queued without a wait), else the waited-for single launches
     kind = "_b2b_us" if any(k.endswith("_b2b_us") for k in scan) else "_us"
@@ -381,7 +385,7 @@ def main():
         per = [None] * world
         dist.all_gather_object(per, mine)
         dist_info["per_rank"] = per
-        pred = shard_time_prediction(n, m, args.family, B, total_B)
+        pred = shard_time_prediction(n, m, args.family, B, total_B, qpb.version())
         if pred:
             dist_info["single_gpu_prediction"] = pred
     gather_ms, gather = None, None

@@ -149,10 +149,12 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   double Lr[NH], E[NP];
   double bv;
   if constexpr (BOX) {
-    // row l < n: x_l <= ub_l; row n + i: -x_i <= -lb_i (absent: +inf)
+    // row l < n: x_l <= ub_l; row n + i: -x_i <= -lb_i.  An absent bound
+    // (NULL array) is ub = +inf / lb = -inf, so both rows get b = +inf (as
+    // gi_box), never a -inf slack
     const int bi = l < n ? l : (l < 2 * n ? l - n : 0);
     const double *bnd = l < n ? bg : Ag;
-    const double v = bnd ? bnd[g * n + bi] : kInf;
+    const double v = bnd ? bnd[g * n + bi] : (l < n ? kInf : -kInf);
     bv = l < n ? v : -v;
     if (!(bv == bv)) bv = kInf;  // NaN bound: absent
   } else {

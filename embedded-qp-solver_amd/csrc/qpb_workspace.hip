@@ -32,6 +32,7 @@ struct Entry {
   std::mutex mu;  // held while the buffer is grown and the launch is queued
   void *p = nullptr;
   size_t bytes = 0;
+  bool dead = false;  // released and erased from the map: look the stream up again
 };
 std::mutex g_mu;  // the map itself
 std::map<std::pair<int, hipStream_t>, std::shared_ptr<Entry>> g_ws;
@@ -39,7 +40,10 @@ std::map<std::pair<int, hipStream_t>, std::shared_ptr<Entry>> g_ws;
 // frees one entry's buffer stream-ordered on its stream and waits for it; the
 // caller holds the entry's lock
 bool free_entry(int dev, hipStream_t st, Entry &w) {
-  if (!w.p) return true;
+  if (!w.p) {
+    w.dead = true;
+    return true;
+  }
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(dev);
@@ -47,6 +51,7 @@ bool free_entry(int dev, hipStream_t st, Entry &w) {
   (void)hipSetDevice(cur);
   w.p = nullptr;
   w.bytes = 0;
+  w.dead = true;
   return ok;
 }
 }  // namespace
@@ -55,14 +60,22 @@ hipError_t qpb_with_workspace(hipStream_t stream, size_t bytes, const std::funct
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
+  // A release may free and erase the entry between the lookup and the entry's
+  // lock: it then marks the entry dead, and the lookup is repeated (a dead
+  // entry is in no map, so a buffer allocated through it would never be freed)
   std::shared_ptr<Entry> sp;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    auto &slot = g_ws[{dev, stream}];
-    if (!slot) slot = std::make_shared<Entry>();
-    sp = slot;
+  std::unique_lock<std::mutex> lock;
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> ml(g_mu);
+      auto &slot = g_ws[{dev, stream}];
+      if (!slot) slot = std::make_shared<Entry>();
+      sp = slot;
+    }
+    lock = std::unique_lock<std::mutex>(sp->mu);
+    if (!sp->dead) break;
+    lock.unlock();
   }
-  std::lock_guard<std::mutex> lock(sp->mu);
   Entry &w = *sp;
   if (w.bytes < bytes) {
     if (w.p) (void)hipFreeAsync(w.p, stream);

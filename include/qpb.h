@@ -135,7 +135,9 @@ int qpb_solve_host(const qpb_desc *desc, const double *H, const double *f,
  * qpb_solve replaces the dense path.  desc->n <= 32 (QPB_ERR_UNSUPPORTED
  * above; pass the dense A = [I; -I] to qpb_solve there); desc->m must be 2n.  lb, ub: B x n, either may be NULL,
  * and +-inf entries are absent bounds.  lam: B x 2n (upper bounds' multipliers
- * first, then the lower bounds'), active: B words in the same row order;
+ * first, then the lower bounds'); active: B x ceil(2n/32) uint32 words in the
+ * same row order -- ONE word per QP for n <= 16, TWO for 16 < n <= 32 (size
+ * it as qpb_solve's ceil(m/32) with m = 2n; the n > 16 kernel writes both);
  * x, status, iters as qpb_solve.  Device pointers; asynchronous on `stream`. */
 int qpb_solve_box(const qpb_desc *desc, const double *H, const double *f,
 		  const double *lb, const double *ub, double *x, double *lam,

@@ -97,3 +97,17 @@ def test_cpu_run_before_gpu_init_is_allowed(bench, monkeypatch):
     monkeypatch.setitem(sys.modules, "torch", fake)
     # no reference library under this name: returns None without forking
     assert bench.cpu_run("ref_admm_batch", 1, [[0.0]], [0.0], 0.1, 1, lib_name="absent.so") is None
+
+
+def test_shard_prediction_is_keyed_by_kernel_revision(bench):
+    # the N > 1 line's kernel-bound speed-up comes from the committed batch
+    # scan only while the scan names a hot-kernel revision of the loaded
+    # library: a stale scan yields no prediction
+    scan = json.load(open(os.path.join(ROOT, "profiles", "batch_scan.json")))
+    rev = scan["revision"]
+    lib_ok = "qpb x.y (gfx950; " + rev + ": desc; gi_box v1: ...)"
+    got = bench.shard_time_prediction(16, 32, "box", 131072, 1048576, lib_ok)
+    assert got is not None and got["revision"] == rev
+    assert got["kernel_bound_speedup"] == pytest.approx(got["total_kernel_ms"] / got["shard_kernel_ms"])
+    assert bench.shard_time_prediction(16, 32, "box", 131072, 1048576, "qpb (gi_dense v0: x)") is None
+    assert bench.shard_time_prediction(16, 32, "dense", 131072, 1048576, lib_ok) is None

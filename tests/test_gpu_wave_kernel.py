@@ -86,3 +86,31 @@ def test_wave_kernel_config5_full_batch(qpb, family):
         assert _relerr(x[k:k + 1], ref.x[None]).max() <= X_TOL, i
         assert np.array_equal(mask[i], ref.active), i
         assert np.abs(lam[k] - ref.lam).max() / (1 + np.abs(ref.lam).max()) <= X_TOL, i
+
+
+@pytest.mark.parametrize("n,m,kind", [(1, 2, "box"), (7, 14, "dense"), (13, 20, "dense"), (13, 26, "box"),
+                                      (16, 32, "box"), (5, 31, "dense")])
+def test_diag_wave_flag_small_and_odd_sizes(qpb, n, m, kind):
+    """QPB_FLAG_DIAG_WAVE routes n <= 16, m <= 32 to the one-QP-per-wavefront
+    kernel (the group-size-1 endpoint of DESIGN.md §2.1), which otherwise only
+    runs with n > 16 or m > 32: at small and odd shapes its answer
+    matches the oracle (x, lambda within 1e-6, active set bit-exact) and the
+    four-QPs-per-wavefront kernel's active sets on the same QPs."""
+    H, f, A, b = O.family_conditioned(77 + 3 * n + m, 21, n, m=m, box=10.0, kind=kind)
+    dev = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (H, f, A, b)]
+    wave = qpb.solve(*dev, flags=qpb.FLAG_DIAG_WAVE)
+    dense = qpb.solve(*dev)
+    torch.cuda.synchronize()
+    st = wave.status.cpu().numpy()
+    assert (st == qpb.OK).all(), st
+    x, lam = wave.x.cpu().numpy(), wave.lam.cpu().numpy()
+    mask = qpb.active_mask_to_bool(wave.active.cpu().numpy(), m)
+    assert np.array_equal(mask, qpb.active_mask_to_bool(dense.active.cpu().numpy(), m))
+    r = O.kkt_residuals(H, f, A, b, x, lam)
+    assert max(float(v.max()) for v in r.values()) <= 1e-9
+    for i in range(len(f)):
+        ref = O.active_set_solve(H[i], f[i], A[i], b[i])
+        assert ref.status == 0
+        assert _relerr(x[i:i + 1], ref.x[None]).max() <= X_TOL, i
+        assert np.array_equal(mask[i], ref.active), i
+        assert np.abs(lam[i] - ref.lam).max() / (1 + np.abs(ref.lam).max()) <= X_TOL, i

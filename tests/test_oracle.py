@@ -137,3 +137,57 @@ def test_device_kkt_helper_matches_oracle_certificate():
         t = [torch.from_numpy(np.ascontiguousarray(v)) for v in (H, f, A, b, xx, ll)]
         got = kkt_max_residual_device(*t, chunk=4)
         assert abs(got - ref) <= 1e-12 * max(1.0, ref), (got, ref)
+
+
+@pytest.mark.parametrize("name", ["cond_box_n16", "cond_dense_n16_m32", "cond_box_n4", "cond_dense_n4_m8",
+                                  "cond_dense_n10_m20"])
+def test_oracle_rules_reproduce_every_fixture(name):
+    """The oracle with its round-6 rules (full-step flag, Bland's rule after a
+    degenerate step) reproduces every committed constrained fixture: x within
+    1e-9 relative and the active set bit-exact."""
+    g = load(name)
+    for i in range(len(g["f"])):
+        r = O.active_set_solve(g["H"][i], g["f"][i], g["A"][i], g["b"][i])
+        assert r.status == 0, i
+        assert np.abs(r.x - g["x"][i]).max() <= 1e-9 * max(1.0, np.abs(g["x"][i]).max()), i
+        assert np.array_equal(r.active, g["act"][i]), i
+
+
+def _vertex_qp(n, m, seed, k):
+    # one QP of tests/test_gpu_active_set.py's vertex family
+    rs = np.random.default_rng(seed)
+    Bm = rs.standard_normal((256, n, n))
+    H = np.eye(n) + 0.1 * np.einsum("bki,bkj->bij", Bm, Bm) / n
+    f = 100.0 * rs.standard_normal((256, n))
+    A = rs.standard_normal((256, m, n))
+    A /= np.linalg.norm(A, axis=2, keepdims=True)
+    b = rs.uniform(0.1, 1.0, (256, m))
+    return H[k], f[k], A[k], b[k]
+
+
+@pytest.mark.parametrize("n,m,k", [(16, 32, 181), (16, 32, 182), (12, 24, 209), (32, 64, 14)])
+def test_oracle_terminates_at_full_vertices(n, m, k):
+    """QPs of the vertex family on whose path round 5's oracle reached a full
+    working set (|W| = n) and then stepped by rounding noise until max_iter:
+    now solved and KKT-certified."""
+    H, f, A, b = _vertex_qp(n, m, 500 + n, k)
+    r = O.active_set_solve(H, f, A, b)
+    assert r.status == 0
+    res = O.kkt_residuals(H[None], f[None], A[None], b[None], r.x[None], r.lam[None])
+    assert max(float(v.max()) for v in res.values()) <= 1e-9
+
+
+def test_oracle_degenerate_vertex_bland():
+    """A degenerate start: 2n rows through the origin (more than n active
+    there, so the first steps are degenerate, alpha = 0); Bland's rule ends
+    them and the answer is KKT-certified."""
+    n = 4
+    rs = np.random.default_rng(3)
+    A = np.abs(rs.standard_normal((2 * n, n))) + 0.1  # a_i > 0: x = 0 is the optimum for f < 0
+    A /= np.linalg.norm(A, axis=1, keepdims=True)
+    b = np.zeros(2 * n)
+    H, f = np.eye(n), -np.ones(n)
+    r = O.active_set_solve(H, f, A, b, x0=np.zeros(n))
+    assert r.status == 0
+    res = O.kkt_residuals(H[None], f[None], A[None], b[None], r.x[None], r.lam[None])
+    assert max(float(v.max()) for v in res.values()) <= 1e-9
