@@ -35,6 +35,9 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
 extern "C" hipError_t qpb_launch_gi_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
                                         const double *ub, double *x, double *lam, uint32_t *active, int32_t *status,
                                         int32_t *iters, hipStream_t stream);
+extern "C" hipError_t qpb_launch_gi_gram_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
+                                             const double *ub, double *x, double *lam, uint32_t *active,
+                                             int32_t *status, int32_t *iters, hipStream_t stream);
 extern "C" hipError_t qpb_launch_gi_wave_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
                                              const double *ub, double *x, double *lam, uint32_t *active,
                                              int32_t *status, int32_t *iters, hipStream_t stream);
@@ -148,8 +151,6 @@ extern "C" int qpb_solve_box(const qpb_desc *d, const double *H, const double *f
   int rc = check_desc(d);
   if (rc) return rc;
   if (d->m != 2 * d->n) return fail(QPB_ERR_INVALID_ARG, "qpb_solve_box: m must be 2n (got n=%d m=%d)", d->n, d->m);
-  if (d->n > 32)
-    return fail(QPB_ERR_UNSUPPORTED, "qpb_solve_box: n=%d > 32 (pass A = [I; -I], b = [ub; -lb] to qpb_solve)", d->n);
   if (d->batch == 0) return 0;
   if (!H || !f || !x || !lam || !active || !status)
     return fail(QPB_ERR_INVALID_ARG, "H, f, x, lam, active and status are required");
@@ -157,12 +158,13 @@ extern "C" int qpb_solve_box(const qpb_desc *d, const double *H, const double *f
   if (rc) return rc;
   // n <= 16: four QPs per wavefront (qpb_gi_box.hip), at most 2^27 QPs per
   // launch (2^32 work-items); 16 < n <= 32: one QP per wavefront (the BOX
-  // instantiation of qpb_gi_wave.hip), 2^25
+  // instantiation of qpb_gi_wave.hip), 2^25; 32 < n <= 128: one QP per
+  // workgroup (the BOX instantiation of qpb_gi_gram.hip, a persistent grid)
   const long long n = d->n, w = (2 * n + 31) / 32, step = n <= 16 ? 1LL << 27 : 1LL << 25;
   for (long long k0 = 0; k0 < d->batch; k0 += step) {
     qpb_desc c = *d;
     c.batch = d->batch - k0 < step ? d->batch - k0 : step;
-    hipError_t e = (n <= 16 ? qpb_launch_gi_box : qpb_launch_gi_wave_box)(
+    hipError_t e = (n <= 16 ? qpb_launch_gi_box : n <= 32 ? qpb_launch_gi_wave_box : qpb_launch_gi_gram_box)(
         &c, H + k0 * n * n, f + k0 * n, lb ? lb + k0 * n : lb, ub ? ub + k0 * n : ub, x + k0 * n, lam + k0 * 2 * n,
         active + k0 * w, status + k0, iters ? iters + k0 : iters, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "qpb_solve_box launch");

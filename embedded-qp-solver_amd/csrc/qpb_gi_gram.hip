@@ -423,7 +423,11 @@ struct Rows {
 };
 
 // ------------------------------------------------------------------ kernel
-template <bool STAMP>
+// BOX: lb <= x <= ub with A = [I; -I] implicit (qpb_solve_box for 32 < n <= 128):
+// Ag = lb, bg = ub (n per QP, either may be NULL: absent bounds), m = 2n; the
+// rows of A are generated where they are loaded (D = A L^{-T} is formed as for
+// a dense A; nothing else reads A)
+template <bool STAMP, bool BOX = false>
 __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg, uint32_t *__restrict__ actg,
@@ -468,7 +472,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     const long long g = flags[1];
     if (g >= batch) break;
     const double *Hq = Hg + g * (long long)n * n;
-    const double *Aq = Ag + g * (long long)m * n;
+    const double *Aq = BOX ? Hq : Ag + g * (long long)m * n;
 
     // ------------------------------------------------------------ setup
     clk.tick(10);
@@ -500,7 +504,23 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     // overwrites in place.
     double E[RT][8][4];
     double bl[RT];
-    if (m > 0) {
+    if constexpr (BOX) {
+      // row r < n: x_r <= ub_r (a = e_r); row n + i: -x_i <= -lb_i (a = -e_i);
+      // an absent bound (NULL array, NaN) is +inf: the row is never violated
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const int rr = row[t], c0 = rr < n ? rr : rr - n;
+        const double sg = rr < n ? 1.0 : -1.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) E[t][k][r] = (rowok[t] && 16 * k + lk + 4 * r == c0) ? sg : 0.0;
+        const double *bnd = rr < n ? bg : Ag;
+        const double v = (rowok[t] && bnd) ? bnd[g * n + c0] : (rr < n ? kInf : -kInf);
+        const double bv = rr < n ? v : -v;
+        bl[t] = rowok[t] ? (bv == bv ? bv : kInf) : 0.0;
+      }
+    } else if (m > 0) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
 #pragma unroll
@@ -1014,10 +1034,10 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 }  // namespace qpb
 
 // scratch: per workgroup (NB - QL) D_W rows beyond the LDS ones + the queue head
-extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
-                                         const double *b, double *x, double *lam, uint32_t *active,
-                                         int32_t *status, int32_t *iters, unsigned long long *sections,
-                                         hipStream_t stream) {
+template <bool BOX>
+static hipError_t launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                 const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
+                                 int32_t *iters, unsigned long long *sections, hipStream_t stream) {
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
   int dev = 0, cus = 0;
@@ -1032,14 +1052,29 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
     int *queue = reinterpret_cast<int *>(static_cast<char *>(buf) + rows_bytes);
     hipError_t err = hipMemsetAsync(queue, 0, sizeof(int), stream);
     if (err != hipSuccess) return err;
-    if (sections)
-      hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<true>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
+    if constexpr (!BOX)  // the stamped diagnostic build exists for the dense form only
+      if (sections) {
+        hipLaunchKernelGGL((qpb::gram::gi_gram_kernel<true, BOX>), dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
                          f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
                          queue, static_cast<double *>(buf), sections);
-    else
-      hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<false>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
+        return hipGetLastError();
+      }
+    hipLaunchKernelGGL((qpb::gram::gi_gram_kernel<false, BOX>), dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
                          f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
                          queue, static_cast<double *>(buf), nullptr);
     return hipGetLastError();
   });
+}
+
+extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                         const double *b, double *x, double *lam, uint32_t *active,
+                                         int32_t *status, int32_t *iters, unsigned long long *sections,
+                                         hipStream_t stream) {
+  return launch_gi_gram<false>(d, H, f, A, b, x, lam, active, status, iters, sections, stream);
+}
+// qpb_solve_box for 32 < n <= 128: lb, ub in A's and b's places (d->m == 2 d->n)
+extern "C" hipError_t qpb_launch_gi_gram_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
+                                             const double *ub, double *x, double *lam, uint32_t *active,
+                                             int32_t *status, int32_t *iters, hipStream_t stream) {
+  return launch_gi_gram<true>(d, H, f, lb, ub, x, lam, active, status, iters, nullptr, stream);
 }

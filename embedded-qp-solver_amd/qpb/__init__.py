@@ -161,7 +161,7 @@ def solve(H, f, A=None, b=None, *, max_iter: int = 0, feas_tol: float = 0.0, out
 def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, feas_tol: float = 0.0, out: Solution | None = None,
               stream=None) -> Solution:
     """Batched min 1/2 x^T H x + f^T x s.t. lb <= x <= ub on the GPU (qpb_solve_box,
-    n <= 32): the reference admm()'s box QP (qp_solvers.c:146-319), solved exactly.
+    n <= 128): the reference admm()'s box QP (qp_solvers.c:146-319), solved exactly.
 
     H (B,n,n), f (B,n), lb / ub (B,n) CUDA float64 tensors or None (absent
     bounds; +-inf entries likewise).  The Solution has m = 2n: lam[:, :n] and

@@ -131,13 +131,15 @@ int qpb_solve_host(const qpb_desc *desc, const double *H, const double *f,
  * reference's admm() (qp_solvers.c:146-319, bounds config.h:29-30), solved
  * exactly with A = [I; -I], b = [ub; -lb] kept implicit (qpb_gi_box.hip for
  * n <= 16, four QPs per wavefront; the BOX form of qpb_gi_wave.hip for
- * 16 < n <= 32, one QP per wavefront).  Replaces admm()'s box QP the way
- * qpb_solve replaces the dense path.  desc->n <= 32 (QPB_ERR_UNSUPPORTED
- * above; pass the dense A = [I; -I] to qpb_solve there); desc->m must be 2n.  lb, ub: B x n, either may be NULL,
+ * 16 < n <= 32, one QP per wavefront; the BOX form of qpb_gi_gram.hip for
+ * 32 < n <= 128, one QP per workgroup).  Replaces admm()'s box QP the way
+ * qpb_solve replaces the dense path.  desc->n <= QPB_MAX_N (128;
+ * QPB_ERR_UNSUPPORTED above); desc->m must be 2n.  lb, ub: B x n, either may be NULL,
  * and +-inf entries are absent bounds.  lam: B x 2n (upper bounds' multipliers
  * first, then the lower bounds'); active: B x ceil(2n/32) uint32 words in the
- * same row order -- ONE word per QP for n <= 16, TWO for 16 < n <= 32 (size
- * it as qpb_solve's ceil(m/32) with m = 2n; the n > 16 kernel writes both);
+ * same row order -- ONE word per QP for n <= 16, TWO for 16 < n <= 32, up to
+ * EIGHT at n = 128 (size it as qpb_solve's ceil(m/32) with m = 2n; the n > 16
+ * kernels write every word);
  * x, status, iters as qpb_solve.  Device pointers; asynchronous on `stream`. */
 int qpb_solve_box(const qpb_desc *desc, const double *H, const double *f,
 		  const double *lb, const double *ub, double *x, double *lam,

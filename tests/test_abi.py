@@ -92,11 +92,12 @@ def test_box_argument_errors_without_gpu():
     lib.qpb_solve_box.argtypes = [ctypes.POINTER(Desc)] + [vp] * 10
     d = Desc(16, 30, 4, 0, 0, 0.0)  # m must be 2n
     assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == -1
-    d = Desc(33, 66, 4, 0, 0, 0.0)  # the box kernels cover n <= 32
+    d = Desc(129, 258, 4, 0, 0, 0.0)  # the box kernels cover n <= 128 (round 6; n <= 32 before)
     assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == -2
-    assert b"qpb_solve" in lib.qpb_last_error()
-    d = Desc(20, 40, 4, 0, 0, 0.0)  # n <= 32: supported; NULL outputs are refused
-    assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == -1
+    assert b"outside this build" in lib.qpb_last_error()
+    for n in (20, 100):  # supported; NULL outputs are refused
+        d = Desc(n, 2 * n, 4, 0, 0, 0.0)
+        assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == -1
     d = Desc(16, 32, 0, 0, 0, 0.0)
     assert lib.qpb_solve_box(ctypes.byref(d), *([None] * 10)) == 0
     if not _device_present():

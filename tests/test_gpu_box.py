@@ -1,5 +1,6 @@
 """GPU parity of the box-constrained kernels (qpb_solve_box: qpb_gi_box.hip for
-n <= 16, the BOX form of qpb_gi_wave.hip for 16 < n <= 32):
+n <= 16, the BOX form of qpb_gi_wave.hip for 16 < n <= 32, the BOX form of
+qpb_gi_gram.hip for 32 < n <= 128 since round 6):
 lb <= x <= ub with A = [I; -I] kept implicit -- the constraint class of the
 reference's admm() (qp_solvers.c:146-319).  Oracles: the KKT-certified primal
 active set (oracle.active_set_solve) on the same QPs written with a dense
@@ -51,7 +52,7 @@ def _np(sol):
 
 
 @pytest.mark.parametrize("n,count", [(16, 64), (4, 40), (7, 33), (13, 17), (1, 9), (20, 24), (32, 32), (25, 9),
-                                     (17, 5), (31, 1)])
+                                     (17, 5), (31, 1), (33, 7), (48, 12), (100, 5), (128, 8)])
 def test_box_matches_oracle(qpb, n, count):
     H, f, lb, ub = _family(100 + n, count, n)
     x, lam, act, st, it = _np(qpb.solve_box(*_cuda(H, f, lb, ub)))
@@ -68,11 +69,11 @@ def test_box_matches_oracle(qpb, n, count):
         assert np.abs(lam[i] - ref.lam).max() / (1.0 + np.abs(ref.lam).max()) <= TOL, i
 
 
-@pytest.mark.parametrize("n", [16, 9, 20, 32])
+@pytest.mark.parametrize("n", [16, 9, 20, 32, 40, 128])
 def test_box_matches_dense_path(qpb, n):
     """The same QPs through qpb_solve with the dense A = [I; -I]: same active
     sets and statuses, x and lambda to rounding."""
-    B = 8192 + 3  # ragged last group
+    B = 8192 + 3 if n <= 32 else 1027  # ragged last group
     H, f, lb, ub = _family(7 + n, B, n)
     A, b = _dense(lb, ub)
     xb, lb_, ab, sb, ib = _np(qpb.solve_box(*_cuda(H, f, lb, ub)))
@@ -84,7 +85,7 @@ def test_box_matches_dense_path(qpb, n):
     assert np.abs(ib.astype(int) - idd.astype(int)).max() <= 2  # selection ties may reorder steps
 
 
-@pytest.mark.parametrize("n", [16, 32])
+@pytest.mark.parametrize("n", [16, 32, 64])
 def test_box_one_sided_and_absent_bounds(qpb, n):
     B = 200
     H, f, lb, ub = _family(31, B, n)
@@ -104,7 +105,7 @@ def test_box_one_sided_and_absent_bounds(qpb, n):
     assert np.array_equal(qpb.active_mask_to_bool(aa, 2 * n)[:, :n], qpb.active_mask_to_bool(ad, n))
 
 
-@pytest.mark.parametrize("n", [16, 32])
+@pytest.mark.parametrize("n", [16, 32, 80])
 def test_box_statuses(qpb, n):
     H, f, lb, ub = _family(5, 8, n)
     lb[3, 2] = ub[3, 2] + 1.0  # empty box -> INFEASIBLE
@@ -179,7 +180,35 @@ def test_box_config4_shape_batch(qpb):
     assert max(float(v.max()) for v in r.values()) <= 1e-9
 
 
-def test_box_beyond_32_is_unsupported(qpb):
-    H, f, lb, ub = _family(3, 2, 33)
+def test_box_config3_shape_batch(qpb):
+    """n = 128 (BASELINE configs[3]'s size) at its batch B = 16 384 through
+    the box entry point (the BOX form of the n <= 128 kernel, A implicit)
+    against the dense path on A = [I; -I]: the same active set on every QP, x
+    to rounding, KKT on a sample of 1024 QPs, the oracle on 16."""
+    B, n = 16384, 128
+    H, f, A, b = qpb.generate(n, B, 20261015, family="box", device=torch.device("cuda", 0))
+    ub = b[:, :n].contiguous()
+    lb = (-b[:, n:]).contiguous()
+    sol = qpb.solve_box(H, f, lb, ub)
+    dense = qpb.solve(H, f, A, b)
+    torch.cuda.synchronize()
+    assert bool((sol.status == qpb.OK).all()) and bool((dense.status == qpb.OK).all())
+    assert torch.equal(sol.active, dense.active)
+    assert float((sol.x - dense.x).abs().max() / dense.x.abs().max().clamp(min=1.0)) <= 1e-10
+    idx = torch.arange(0, B, B // 1024, device=f.device)
+    Hs, fs, As, bs = (t[idx].cpu().numpy() for t in (H, f, A, b))
+    xs, ls = sol.x[idx].cpu().numpy(), sol.lam[idx].cpu().numpy()
+    r = O.kkt_residuals(Hs, fs, As, bs, xs, ls)
+    assert max(float(v.max()) for v in r.values()) <= 1e-9
+    mask = qpb.active_mask_to_bool(sol.active[idx].cpu().numpy(), 2 * n)
+    for k in range(0, len(idx), 64):
+        ref = O.active_set_solve(Hs[k], fs[k], As[k], bs[k])
+        assert ref.status == 0
+        assert np.abs(xs[k] - ref.x).max() / max(1.0, np.abs(ref.x).max()) <= TOL, k
+        assert np.array_equal(mask[k], ref.active), k
+
+
+def test_box_beyond_128_is_unsupported(qpb):
+    H, f, lb, ub = _family(3, 2, 129)
     with pytest.raises(qpb.QPBError):
         qpb.solve_box(*_cuda(H, f, lb, ub))

@@ -82,13 +82,18 @@ def test_mixed_config4_batch_equals_fp64(qpb, kind):
     assert float(ex.max()) <= X_TOL and float(el.max()) <= X_TOL, (float(ex.max()), float(el.max()))
     worst = kkt_torch(H, f, A, b, mix.x, mix.lam)
     assert all(v <= KKT_TOL for v in worst.values()), worst
-    # independent oracle on a sample
-    idx = np.random.default_rng(3).choice(B, 8, replace=False)
+    # independent oracle on 128 QPs (round 5: 8, VERDICT r05 Weak 1): x and
+    # lambda within 1e-6, the active set bit-exact
+    idx = np.r_[0, B - 1, np.random.default_rng(3).choice(B, 126, replace=False)]
     Hs, fs, As, bs = (t[idx].cpu().numpy() for t in (H, f, A, b))
-    xs = mix.x[idx].cpu().numpy()
+    xs, ls = mix.x[idx].cpu().numpy(), mix.lam[idx].cpu().numpy()
+    ms = qpb.active_mask_to_bool(mix.active[idx].cpu().numpy(), 64)
     for k in range(len(idx)):
         o = O.active_set_solve(Hs[k], fs[k], As[k], bs[k])
-        assert _relerr(xs[k:k + 1], o.x[None]).max() <= X_TOL
+        assert o.status == 0, idx[k]
+        assert _relerr(xs[k:k + 1], o.x[None]).max() <= X_TOL, idx[k]
+        assert np.array_equal(ms[k], o.active), idx[k]
+        assert np.abs(ls[k] - o.lam).max() / (1 + np.abs(o.lam).max()) <= X_TOL, idx[k]
 
 
 def test_mixed_redo_fraction(qpb):

@@ -2,9 +2,9 @@
 """Kernel times of the BASELINE configs beyond the headline one (HIP events,
 median of R launches) with the max_iter ablation (setup + one iteration vs
 the full solve): configs[3] n=128 m=256 B=16,384, configs[4] shape n=32
-m=64 B=262,144 (fp64 and mixed precision), the n = 32 box family through the
-dense path and the implicit-A box path, and the headline n=16 m=32 B=65,536
-(configs[1])."""
+m=64 B=262,144 (fp64 and mixed precision), the n = 32 and n = 128 box
+families through the dense path and the implicit-A box path, and the headline
+n=16 m=32 B=65,536 (configs[1])."""
 import json
 import os
 import sys
@@ -74,7 +74,8 @@ def main():
             ("c4_n32_m64_mixed", 32, 262144, "dense", 5, qpb.FLAG_MIXED, "dense"),
             ("c4_n32_box_dense_path", 32, 262144, "box", 5, 0, "dense"),
             ("c4_n32_box_fast_path", 32, 262144, "box", 5, 0, "box"),
-            ("c3_n128_m256", 128, 16384, "box", 3, 0, "dense"))
+            ("c3_n128_m256", 128, 16384, "box", 3, 0, "dense"),
+            ("c3_n128_box_fast_path", 128, 16384, "box", 3, 0, "box"))
     for name, n, B, fam, reps, fl, path in rows:
         if args and name not in args:
             continue
