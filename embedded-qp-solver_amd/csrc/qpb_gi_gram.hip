@@ -172,71 +172,21 @@ __device__ __forceinline__ void row_dot(const double (&E)[RT][8][4], const doubl
 // symmetric packed access
 __device__ __forceinline__ double sym(const double *P, int i, int j) { return i >= j ? P[tri(i, j)] : P[tri(j, i)]; }
 
-// ------------------------------------------------- Cholesky + D = A L^{-T}
+// ---------------------------------------------------------------- Cholesky
 // H (n x n, padded to 16 T with the identity) from global memory into the
 // packed lower triangle, factorised in place: blocked right-looking over
-// 16 x 16 tiles.  A diagonal tile is factorised by one wavefront (lane i owns
+// 16 x 16 tiles.  The diagonal tile is factorised by wavefront 0 (lane i owns
 // row i, pivot rows by DPP broadcast as in qpb_gi.hip) and inverted (lane j
 // solves column j); the panel below it is multiplied by that inverse and the
-// trailing tiles updated on the matrix cores.
-//
-// D = A L^{-T} and y = L^{-1} f are formed INSIDE the factorisation (gi_gram
-// v4.6, round 6): column block k of D (16 columns of the wave's 32 rows) and
-// block k of y need only L's block row k and the inverse of diagonal tile k,
-// both final once tile k is factorised, so every wavefront computes its
-// block k in step k while wavefront 0 factorises tile k + 1 (one wavefront's
-// dependent pivot chain, about 2.3 us per tile: the critical path).  Round 5
-// ran the 26 us chain first, then D on the matrix cores (26.8 us) and y on
-// one wavefront (the last solve of the setup); the chain now hides most of
-// D.  The steps are unrolled so that E[t][k] is indexed statically; the A
-// operand of block k + 1 is loaded at the start of step k into the registers
-// that become D.  The tile sweep keeps each row on two DPP rows (even / odd
-// columns): 32 registers instead of 64 while D's blocks are live, and half
-// the FMAs of the early pivot steps.
-// Returns false if a pivot <= 0.
+// trailing tiles updated on the matrix cores.  Returns false if a pivot <= 0.
 template <class CLK>
-__device__ __forceinline__ bool setup(double *lds, const double *__restrict__ Hq, const double *__restrict__ Aq,
-                                      const double *__restrict__ bq, const double *__restrict__ fq, int n, int m,
-                                      int T, int tid,
-                                      const int (&row)[RT], const bool (&rowok)[RT], double (&E)[RT][8][4],
-                                      double (&bl)[RT], double (&na2)[RT], CLK &clk) {
+__device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__ Hq, const double *__restrict__ fq, int n,
+                                         int T, int tid, CLK &clk) {
   double *Lp = lds + OFF_TRI;
   double *LI = lds + OFF_ROWS;
   int *flags = reinterpret_cast<int *>(lds + B_INT);
   const int l = tid & 63, wv = tid >> 6;  // tid: the caller's opaque thread id
   const int nb = 16 * T;
-  // the lane's tile coordinates, re-derived opaquely wherever used: with the
-  // eight steps unrolled, addresses built from shared lane ids would be
-  // hoisted to the top and kept live (in spill slots) across the whole setup
-  auto lane_ids = [&](int &li, int &lk) {
-    int t = tid;
-    asm volatile("" : "+v"(t));
-    li = t & 15;
-    lk = (t & 63) >> 4;
-  };
-  // block k of A (this lane's entries of its two rows) into E[t][k], raw:
-  // no select and no branch around the loads, so that they stay in flight
-  // until the block is used (a select on the loaded value, or a phi at the
-  // end of a guarded block, makes the compiler wait for the load right
-  // there).  Entries past n or m, and every entry when m = 0 (A may be NULL:
-  // the clamped address then points into H), are masked where the block is
-  // read (d0_block); blocks k >= T are zeroed after the last step.
-  const double *Ab = m > 0 ? Aq : Hq;
-  auto load_a = [&](auto Kc) {
-    constexpr int k = Kc;
-    int li, lk;
-    lane_ids(li, lk);
-    (void)li;
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = 16 * k + lk + 4 * r;
-        const bool ok = rowok[t] && col < n;
-        E[t][k][r] = Ab[ok ? row[t] * n + col : 0];
-      }
-  };
-  auto a_ok = [&](int t, int col) { return m > 0 && rowok[t] && col < n; };
   {
     // rows wv, wv + 8, ... (lanes along the columns: coalesced); every load
     // is issued before the first store, one memory round trip per QP.  The
@@ -264,25 +214,42 @@ __device__ __forceinline__ bool setup(double *lds, const double *__restrict__ Hq
       }
     }
   }
+#ifdef GY
   // f into yb (permuted layout, zero past n): y = L^{-1} f is formed in place, block by block
   double *yb = lds + B_Y;
   if (wv == 4) {
     yb[pad(perm(l))] = l < n ? fq[l] : 0.0;
     yb[pad(perm(l + 64))] = l + 64 < n ? fq[l + 64] : 0.0;
   }
+  // block k of y = L^{-1} f (wave 4, in step k: L's block row k and tile k's
+  // inverse are final, and so are y's blocks j < k): lane (g, i) sums its
+  // quarter of L[16k + i, j] y_j over j < 16k, the four quarters are added,
+  // then y_k = Linv_k (f_k - sum), the sum read from lane i by the FMAs
+  auto y_block = [&](int k) {
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    const int i = t & 15, g4 = (t >> 4) & 3;
+    double p0 = 0.0, p1 = 0.0;
+    for (int jj = 0; jj < 4 * k; jj += 2) {
+      const int j0 = 4 * jj + g4, j1 = j0 + 4;
+      p0 = __builtin_fma(Lp[tri(16 * k + i, j0)], yb[pad(perm(j0))], p0);
+      p1 = __builtin_fma(Lp[tri(16 * k + i, j1)], yb[pad(perm(j1))], p1);
+    }
+    const double acc = yb[pad(perm(16 * k + i))] - group_sum(p0 + p1);
+    dpp_ready(acc);
+    double y0 = 0.0, y1 = 0.0;
+    unroll<16>([&](auto Ic) {
+      constexpr int ii = Ic;
+      if constexpr (ii % 2 == 0) fmac_bc<ii>(y0, acc, LI[k * LIT + i * LIS + ii]);
+      if constexpr (ii % 2 == 1) fmac_bc<ii>(y1, acc, LI[k * LIT + i * LIS + ii]);
+    });
+    if (g4 == 0) yb[pad(perm(16 * k + i))] = y0 + y1;
+  };
+#endif
   if (tid == 0) flags[0] = 0;
   __syncthreads();
   clk.tick(11);
-  // A's block 0 and b, in flight under tile 0's factorisation (issued after
-  // H's round trip: loads return in order, so waiting for H's would wait for these)
-  load_a(std::integral_constant<int, 0>{});
-  double braw[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    braw[t] = (m > 0 ? bq : Hq)[rowok[t] ? row[t] : 0];
-    na2[t] = 0.0;
-  }
-  // the diagonal tile K, on the wavefront calling it
+#ifdef G2H
   // The tile's rows are split over two DPP rows: lane i (half 0) holds the
   // even columns 2jj of row i, lane 16 + i (half 1) the odd columns 2jj + 1
   // (lanes 32-63 repeat them; their stores are the same values).  Per step the
@@ -359,11 +326,66 @@ __device__ __forceinline__ bool setup(double *lds, const double *__restrict__ Hq
     }
     if ((t & 63) == 0 && !ok) flags[0] = 1;
   };
+#else
+  // the diagonal tile K, on wavefront 0
+  auto factor_diag = [&](int K) {
+    int i = l & 15;
+    asm volatile("" : "+v"(i));  // opaque per step: nothing lane-dependent is hoisted and kept live
+    const int r0 = 16 * K;
+    // lane i: row i of the tile (a, the full symmetric row) and row i of
+    // the identity (e): the sweep turns e into row i of L^{-T}, i.e.
+    // column i of the tile inverse, alongside the factorisation
+    double a[16], e[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      a[j] = j <= i ? Lp[tri(r0 + i, r0 + j)] : Lp[tri(r0 + j, r0 + i)];
+      e[j] = j == i ? 1.0 : 0.0;
+    }
+    bool ok = true;
+    unroll<16>([&](auto Kc) {
+      constexpr int k = Kc;
+      // a step boundary the scheduler keeps (as qpb_gi.hip's sweep): the
+      // previous step's writes of a[j] (and, at k = 0, the selects above)
+      // stay ahead of this step's broadcast and rsq chain, well over the two
+      // wait states the v_fmac_f64_dpp reads of a[j] need (hipcc does not pad
+      // inline asm; tests/test_dpp_hazards.py checks the built objects)
+      __builtin_amdgcn_sched_barrier(0);
+      // pivot row k of the Schur complement = column k (symmetry): lane k's
+      // entries, broadcast by DPP
+      const double akk = bc<k>(a[k]);
+      ok = ok && (akk > 0.0);
+      const double ik = rsq1(akk);  // hardware estimate + one Newton step (qpb_common.h)
+      const double ik2 = ik * ik;
+      const double c = a[k] * ik2;
+      const double ne2 = -(e[k] * ik2);
+      e[k] *= ik;
+      const double nc = -c;
+      // broadcasts fused into v_fmac_f64_dpp (the pivot row read straight
+      // from lane k); the e update reads lane k's a[j] before the a update of
+      // the same j writes it (volatile asm keeps the order); a[j] was last
+      // written in the previous step, well over two instructions before (the
+      // DPP read hazard)
+      unroll<15 - k>([&](auto J) {
+        constexpr int j = k + 1 + J;
+        fmac_bc<k>(e[j], a[j], ne2);
+        fmac_bc<k>(a[j], a[j], nc);
+      });
+      a[k] *= ik;
+    });
+    if (l < 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j <= i) Lp[tri(r0 + i, r0 + j)] = a[j];
+        LI[K * LIT + j * LIS + i] = e[j];
+      }
+    }
+    if (l == 0 && !ok) flags[0] = 1;
+      };
+#endif
+  const int li = l & 15, lk = l >> 4;
   // one tile update (I, J) -= L[I, K] L[J, K]^T on the matrix cores (two
   // tiles at a time: independent MFMA chains); `on` masks the second one
   auto tile_update2 = [&](int K, const int (&I)[2], const int (&J)[2], const bool (&on)[2]) {
-    int li, lk;
-    lane_ids(li, lk);
     d4 acc[2];
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2)
@@ -385,81 +407,13 @@ __device__ __forceinline__ bool setup(double *lds, const double *__restrict__ Hq
         if (on[h2] && row >= col) Lp[tri(row, col)] = acc[h2][r];
       }
   };
-  // column block k of D for this wave's rows: tile k of D^T (16 columns of D x
-  // 16 rows) = (A^T's tile - sum_{j<k} L[k, j] D^T[j]) times Linv_k; the two
-  // row tiles share every L operand.  |a_row|^2 accumulates on the way.
-  auto d0_block = [&](auto Kc) {
-    constexpr int k = Kc;
-    int li, lk;
-    lane_ids(li, lk);
-    d4 C[RT];
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        C[t][r] = a_ok(t, 16 * k + lk + 4 * r) ? E[t][k][r] : 0.0;
-        na2[t] = __builtin_fma(C[t][r], C[t][r], na2[t]);
-      }
-#pragma unroll
-    for (int j = 0; j < k; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const double a = -Lp[tri(16 * k + li, 16 * j + 4 * s + lk)];
-#pragma unroll
-        for (int t = 0; t < RT; ++t) mfma(a, E[t][j][s], C[t]);
-      }
-    d4 Z[RT];
-#pragma unroll
-    for (int t = 0; t < RT; ++t) Z[t] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const double a = LI[k * LIT + li * LIS + 4 * s + lk];
-#pragma unroll
-      for (int t = 0; t < RT; ++t) mfma(a, C[t][s], Z[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) E[t][k][r] = Z[t][r];
-  };
-  // block k of y = L^{-1} f (wave 4, in step k: L's block row k and tile k's
-  // inverse are final, and so are y's blocks j < k): lane (g, i) sums its
-  // quarter of L[16k + i, j] y_j over j < 16k, the four quarters are added,
-  // then y_k = Linv_k (f_k - sum), the sum read from lane i by the FMAs
-  auto y_block = [&](auto Kc) {
-    constexpr int k = Kc;
-    int t = tid;
-    asm volatile("" : "+v"(t));
-    const int i = t & 15, g4 = (t >> 4) & 3;
-    double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-    for (int jj = 0; jj < 4 * k; jj += 2) {
-      const int j0 = 4 * jj + g4, j1 = j0 + 4;
-      p0 = __builtin_fma(Lp[tri(16 * k + i, j0)], yb[pad(perm(j0))], p0);
-      p1 = __builtin_fma(Lp[tri(16 * k + i, j1)], yb[pad(perm(j1))], p1);
-    }
-    const double acc = yb[pad(perm(16 * k + i))] - group_sum(p0 + p1);
-    dpp_ready(acc);
-    double y0 = 0.0, y1 = 0.0;
-    unroll<16>([&](auto Ic) {
-      constexpr int ii = Ic;
-      if constexpr (ii % 2 == 0) fmac_bc<ii>(y0, acc, LI[k * LIT + i * LIS + ii]);
-      if constexpr (ii % 2 == 1) fmac_bc<ii>(y1, acc, LI[k * LIT + i * LIS + ii]);
-    });
-    if (g4 == 0) yb[pad(perm(16 * k + i))] = y0 + y1;
-  };
   if (wv == 0) factor_diag(0);
   __syncthreads();
-  unroll<8>([&](auto Kc) {
-    constexpr int K = Kc;
+  for (int K = 0; K < T; ++K) {
     clk.tick(12);
-    // A's block K + 1, one step ahead of its use
-    if constexpr (K + 1 < 8) load_a(std::integral_constant<int, K + 1>{});
     // panel: L[I, K] = H~[I, K] Linv_K^T, one tile per wavefront
     if (wv < T - K - 1) {
       const int I = K + 1 + wv;
-      int li, lk;
-      lane_ids(li, lk);
       d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -469,9 +423,13 @@ __device__ __forceinline__ bool setup(double *lds, const double *__restrict__ Hq
     }
     __syncthreads();
     clk.tick(13);
+#ifdef GY
+    if (wv == 4) y_block(K);
+#endif
     if (K + 1 < T) {
-      // look-ahead: wavefront 0 updates the next diagonal tile and
-      // factorises it while the others update the rest of the trailing matrix
+      // look-ahead: wavefront 0 updates the next diagonal tile and factorises
+      // it while the others update the rest of the trailing matrix
+      const int nr = T - K - 1, ntile = nr * (nr + 1) / 2 - 1;  // all but (K+1, K+1)
       if (wv == 0) {
         const int I[2] = {K + 1, K + 1}, J[2] = {K + 1, K + 1};
         const bool on[2] = {true, false};
@@ -479,7 +437,8 @@ __device__ __forceinline__ bool setup(double *lds, const double *__restrict__ Hq
         wave_lds_sync();
         factor_diag(K + 1);
       } else if (wv != 4) {
-        const int nr = T - K - 1, ntile = nr * (nr + 1) / 2 - 1;  // all but (K+1, K+1)
+        // waves 1-3, 5-7: wave 4 shares wavefront 0's SIMD and stays idle, so
+        // the diagonal factorisation (the critical path) keeps its issue slots
         const int wr = wv < 4 ? wv - 1 : wv - 2;
         constexpr int NTW = NWV - 2;
         for (int t0 = wr; t0 < ntile; t0 += 2 * NTW) {
@@ -500,58 +459,70 @@ __device__ __forceinline__ bool setup(double *lds, const double *__restrict__ Hq
           tile_update2(K, I, J, on);
         }
       }
+      __syncthreads();
     }
-    // block K of D on every wave (tile K's inverse and L's block row K are final)
-    if (K < T) {
-      if (wv == 4) y_block(std::integral_constant<int, K>{});
-      d0_block(std::integral_constant<int, K>{});
-    }
-    __syncthreads();
     clk.tick(14);
-  });
-  // blocks past T were loaded raw (or not computed): D is zero there
-#pragma unroll
-  for (int k = 1; k < 8; ++k)
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) E[t][k][r] = k < T ? E[t][k][r] : 0.0;
-#pragma unroll
-  for (int t = 0; t < RT; ++t) bl[t] = (m > 0 && rowok[t]) ? braw[t] : 0.0;
+  }
   return flags[0] == 0;
 }
 
-// Lane-parallel triangular solve with the packed L on one wavefront: lane l
+// Lane-parallel triangular solves with the packed L on one wavefront: lane l
 // owns entries l and l + 64 (a0, a1: right-hand side in, solution out).
 // Step i broadcasts the finished entry i (v_readlane with a constant lane) and
-// every earlier entry takes its update; the steps are unrolled over the whole
-// padded size (entries past nb have zero rows), so only the broadcast chain is
-// serial.  A finished entry is never touched again, so the solution is the
-// accumulator times 1 / L_ii at the end.  (y = L^{-1} f is formed block by
-// block inside the setup since round 6.)
-// L^T x = v (backward); L prefetched 8 steps at a time
+// every later entry takes its update; the steps are unrolled over the whole
+// padded size (entries past nb have zero rows), L prefetched 16 steps at a
+// time, so only the broadcast chain is serial.  A finished entry is never
+// touched again (its later coefficients are zero), so the solution is the
+// accumulator times 1 / L_ii at the end.
+__device__ __forceinline__ void solve_lower(const double *Lp, int nb, int l, double &a0, double &a1) {
+  const double id0 = l < nb ? rcp(Lp[tri(l, l)]) : 0.0;
+  const double id1 = l + 64 < nb ? rcp(Lp[tri(l + 64, l + 64)]) : 0.0;
+  unroll<8>([&](auto C) {
+    constexpr int i0 = 16 * C;
+    double L0[16], L1[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int i = i0 + jj;
+      L0[jj] = (i0 < 64 && l > i && l < nb) ? Lp[tri(l, i)] : 0.0;
+      L1[jj] = (l + 64 > i && l + 64 < nb) ? Lp[tri(l + 64, i)] : 0.0;
+    }
+    unroll<16>([&](auto J) {
+      constexpr int i = i0 + J;
+      if constexpr (i < 64) {
+        const double yi = readlane_d(a0 * id0, i);
+        a0 = __builtin_fma(-L0[J], yi, a0);
+        a1 = __builtin_fma(-L1[J], yi, a1);
+      } else {
+        const double yi = readlane_d(a1 * id1, i - 64);
+        a1 = __builtin_fma(-L1[J], yi, a1);
+      }
+    });
+  });
+  a0 *= id0;
+  a1 *= id1;
+}
+// L^T x = v (backward)
 __device__ __forceinline__ void solve_upper(const double *Lp, int nb, int l, double &a0, double &a1) {
   const double id0 = l < nb ? rcp(Lp[tri(l, l)]) : 0.0;
   const double id1 = l + 64 < nb ? rcp(Lp[tri(l + 64, l + 64)]) : 0.0;
-  unroll<16>([&](auto C) {
-    constexpr int i1 = 120 - 8 * C;
-    __builtin_amdgcn_sched_barrier(0);  // keeps each chunk's loads in it
-    double L0[8], L1[8];
+  unroll<8>([&](auto C) {
+    constexpr int i1 = 112 - 16 * C;
+    double L0[16], L1[16];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
+    for (int jj = 0; jj < 16; ++jj) {
       const int i = i1 + jj;
       L0[jj] = (l < i && i < nb) ? Lp[tri(i, l)] : 0.0;
       L1[jj] = (i1 >= 64 && l + 64 < i && i < nb) ? Lp[tri(i, l + 64)] : 0.0;
     }
-    unroll<8>([&](auto J) {
-      constexpr int i = i1 + 7 - J;
+    unroll<16>([&](auto J) {
+      constexpr int i = i1 + 15 - J;
       if constexpr (i >= 64) {
         const double xi = readlane_d(a1 * id1, i - 64);
-        a0 = __builtin_fma(-L0[7 - J], xi, a0);
-        a1 = __builtin_fma(-L1[7 - J], xi, a1);
+        a0 = __builtin_fma(-L0[15 - J], xi, a0);
+        a1 = __builtin_fma(-L1[15 - J], xi, a1);
       } else {
         const double xi = readlane_d(a0 * id0, i);
-        a0 = __builtin_fma(-L0[7 - J], xi, a0);
+        a0 = __builtin_fma(-L0[15 - J], xi, a0);
       }
     });
   });
@@ -579,6 +550,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
   // 9 x, 10 queue)
   SectionClock<STAMP> clk;
   double *Lp = lds + OFF_TRI;  // L, then Z = R^{-1} (packed by columns)
+  double *LI = lds + OFF_ROWS;
   double *wb = lds + B_W, *vb = lds + B_V, *rb = lds + B_R, *lamb = lds + B_LAM, *yb = lds + B_Y;
   double *red = lds + B_RED;
   int *flags = reinterpret_cast<int *>(lds + B_INT);
@@ -615,11 +587,7 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 
     // ------------------------------------------------------------ setup
     clk.tick(10);
-    // this lane's rows of D (A's entries, then D = A L^{-T} in place), b,
-    // |a_row|^2, and L in the triangle (setup above)
-    double E[RT][8][4];
-    double bl[RT], na2[RT];
-    const bool spd = setup(lds, Hq, Aq, m > 0 ? bg + g * m : Hq, fg + g * n, n, m, T, tid, row, rowok, E, bl, na2, clk);
+    const bool spd = cholesky(lds, Hq, fg + g * n, n, T, tid, clk);
 #ifdef GRAM_ONLY_CHOL
     if (tid == 0) statg[g] = spd;
     continue;
@@ -633,6 +601,88 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       if (e < tri(nb, 0)) Lgl[e] = Lp[e];
     }
     clk.tick(0);
+    // y = L^{-1} f on wavefront 0, into yb (permuted), before D is live
+#ifndef GY
+    if (wv == 0) {
+      double a0 = l < n ? fg[g * n + l] : 0.0, a1 = l + 64 < n ? fg[g * n + l + 64] : 0.0;
+      solve_lower(Lp, nb, l, a0, a1);
+      yb[pad(perm(l))] = a0;
+      yb[pad(perm(l + 64))] = a1;
+    }
+#endif
+    // this lane's entries of A and b, all issued before the first use: one
+    // memory round trip.  Loads are unconditional (masked lanes read a
+    // clamped address): a guarded load becomes a branch with its own wait.
+    // A's entries land in the registers of D, which the blocked substitution
+    // overwrites in place.
+    double E[RT][8][4];
+    double bl[RT];
+    if (m > 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = 16 * k + lk + 4 * r;
+            const bool ok = rowok[t] && col < n;
+            const double v = Aq[ok ? row[t] * n + col : 0];
+            E[t][k][r] = ok ? v : 0.0;
+          }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const double v = bg[g * m + (rowok[t] ? row[t] : 0)];
+        bl[t] = rowok[t] ? v : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) E[t][k][r] = 0.0;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) bl[t] = 0.0;
+    }
+
+    // D = A L^{-T} on the matrix cores: tile k of D^T (16 columns of D x 16
+    // rows) = (A^T's tile - sum_{j<k} L[k, j] D^T[j]) times Linv_k; the two
+    // row tiles of the wave share every L operand
+    double na2[RT] = {};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < T) {
+        d4 C[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            C[t][r] = E[t][k][r];
+            na2[t] = __builtin_fma(C[t][r], C[t][r], na2[t]);
+          }
+#pragma unroll
+        for (int j = 0; j < k; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const double a = -Lp[tri(16 * k + li, 16 * j + 4 * s + lk)];
+#pragma unroll
+            for (int t = 0; t < RT; ++t) mfma(a, E[t][j][s], C[t]);
+          }
+        d4 Z[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) Z[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double a = LI[k * LIT + li * LIS + 4 * s + lk];
+#pragma unroll
+          for (int t = 0; t < RT; ++t) mfma(a, C[t][s], Z[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) E[t][k][r] = Z[t][r];
+      }
+    }
     clk.tick(1);
     // |D[row,:]|^2 of the lane's rows (the dependency test's scale, published
     // with the selection key: no |u|^2 reduction in the loop)
