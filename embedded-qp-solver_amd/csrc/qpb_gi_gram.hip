@@ -180,8 +180,7 @@ __device__ __forceinline__ double sym(const double *P, int i, int j) { return i 
 // solves column j); the panel below it is multiplied by that inverse and the
 // trailing tiles updated on the matrix cores.  Returns false if a pivot <= 0.
 template <class CLK>
-__device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__ Hq, const double *__restrict__ fq, int n,
-                                         int T, int tid, CLK &clk) {
+__device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__ Hq, int n, int T, int tid, CLK &clk) {
   double *Lp = lds + OFF_TRI;
   double *LI = lds + OFF_ROWS;
   int *flags = reinterpret_cast<int *>(lds + B_INT);
@@ -214,119 +213,9 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
       }
     }
   }
-#ifdef GY
-  // f into yb (permuted layout, zero past n): y = L^{-1} f is formed in place, block by block
-  double *yb = lds + B_Y;
-  if (wv == 4) {
-    yb[pad(perm(l))] = l < n ? fq[l] : 0.0;
-    yb[pad(perm(l + 64))] = l + 64 < n ? fq[l + 64] : 0.0;
-  }
-  // block k of y = L^{-1} f (wave 4, in step k: L's block row k and tile k's
-  // inverse are final, and so are y's blocks j < k): lane (g, i) sums its
-  // quarter of L[16k + i, j] y_j over j < 16k, the four quarters are added,
-  // then y_k = Linv_k (f_k - sum), the sum read from lane i by the FMAs
-  auto y_block = [&](int k) {
-    int t = tid;
-    asm volatile("" : "+v"(t));
-    const int i = t & 15, g4 = (t >> 4) & 3;
-    double p0 = 0.0, p1 = 0.0;
-    for (int jj = 0; jj < 4 * k; jj += 2) {
-      const int j0 = 4 * jj + g4, j1 = j0 + 4;
-      p0 = __builtin_fma(Lp[tri(16 * k + i, j0)], yb[pad(perm(j0))], p0);
-      p1 = __builtin_fma(Lp[tri(16 * k + i, j1)], yb[pad(perm(j1))], p1);
-    }
-    const double acc = yb[pad(perm(16 * k + i))] - group_sum(p0 + p1);
-    dpp_ready(acc);
-    double y0 = 0.0, y1 = 0.0;
-    unroll<16>([&](auto Ic) {
-      constexpr int ii = Ic;
-      if constexpr (ii % 2 == 0) fmac_bc<ii>(y0, acc, LI[k * LIT + i * LIS + ii]);
-      if constexpr (ii % 2 == 1) fmac_bc<ii>(y1, acc, LI[k * LIT + i * LIS + ii]);
-    });
-    if (g4 == 0) yb[pad(perm(16 * k + i))] = y0 + y1;
-  };
-#endif
   if (tid == 0) flags[0] = 0;
   __syncthreads();
   clk.tick(11);
-#ifdef G2H
-  // The tile's rows are split over two DPP rows: lane i (half 0) holds the
-  // even columns 2jj of row i, lane 16 + i (half 1) the odd columns 2jj + 1
-  // (lanes 32-63 repeat them; their stores are the same values).  Per step the
-  // pivot row still reaches every lane of a half by a fused row_newbcast from
-  // lane k of that half, so a lane updates at most 8 columns per array (16
-  // before): half the FMAs of the early steps and half the registers (32
-  // instead of 64, round 6: this runs while the wave's block rows of D are
-  // live).  The pivot a_kk comes by v_readlane, the row's own column-k
-  // entries (a_ik, e_ik) from the half holding column k by v_permlane16_swap.
-  auto factor_diag = [&](int K) {
-    int t = tid;
-    asm volatile("" : "+v"(t));  // opaque per step: nothing lane-dependent is hoisted and kept live
-    const int i = t & 15, hf = (t >> 4) & 1;
-    const int r0 = 16 * K;
-    // lane (hf, i): columns j = 2 jj + hf of row i of the tile (a, the full
-    // symmetric row) and of row i of the identity (e): the sweep turns e into
-    // row i of L^{-T}, i.e. column i of the tile inverse
-    double a[8], e[8];
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int j = 2 * jj + hf;
-      a[jj] = j <= i ? Lp[tri(r0 + i, r0 + j)] : Lp[tri(r0 + j, r0 + i)];
-      e[jj] = j == i ? 1.0 : 0.0;
-    }
-    bool ok = true;
-    // value v of this row's lane in half H (lanes i, i + 16 swap by v_permlane16_swap)
-    auto from_half = [&](auto Hc, double v) {
-      constexpr int H = Hc;
-      const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-      const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
-      const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-      return __builtin_bit_cast(double, ((unsigned long long)hi[H] << 32) | lo[H]);
-    };
-    unroll<16>([&](auto Kc) {
-      constexpr int k = Kc;
-      constexpr int kr = k >> 1, kh = k & 1;  // column k: register kr of half kh
-      // a step boundary the scheduler keeps (as qpb_gi.hip's sweep): the
-      // previous step's writes of a[jj] stay ahead of this step's pivot chain,
-      // well over the two wait states the v_fmac_f64_dpp reads of a[jj] need
-      // (hipcc does not pad inline asm; tests/test_dpp_hazards.py checks the
-      // built objects)
-      __builtin_amdgcn_sched_barrier(0);
-      const double akk = readlane_d(a[kr], 16 * kh + k);
-      ok = ok && (akk > 0.0);
-      const double ik = rsq1(akk);  // hardware estimate + one Newton step (qpb_common.h)
-      const double ik2 = ik * ik;
-      const double aik = from_half(std::integral_constant<int, kh>{}, a[kr]);
-      const double eik = from_half(std::integral_constant<int, kh>{}, e[kr]);
-      const double nc = -(aik * ik2), ne2 = -(eik * ik2);
-      // columns 2 jj + hf > k: every jj > kr, and jj == kr on half 1 when k is even
-      if constexpr (kh == 0) {
-        const double ncm = hf ? nc : 0.0, nem = hf ? ne2 : 0.0;
-        dpp_ready(ncm);
-        fmac_bc<k>(e[kr], a[kr], nem);
-        fmac_bc<k>(a[kr], a[kr], ncm);
-      }
-      unroll<7 - kr>([&](auto J) {
-        constexpr int jj = kr + 1 + J;
-        fmac_bc<k>(e[jj], a[jj], ne2);
-        fmac_bc<k>(a[jj], a[jj], nc);
-      });
-      // column k itself (half kh): scaled by 1 / sqrt(a_kk)
-      const double sc = hf == kh ? ik : 1.0;
-      e[kr] *= sc;
-      a[kr] *= sc;
-    });
-    if ((t & 63) < 32) {
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int j = 2 * jj + hf;
-        if (j <= i) Lp[tri(r0 + i, r0 + j)] = a[jj];
-        LI[K * LIT + j * LIS + i] = e[jj];
-      }
-    }
-    if ((t & 63) == 0 && !ok) flags[0] = 1;
-  };
-#else
   // the diagonal tile K, on wavefront 0
   auto factor_diag = [&](int K) {
     int i = l & 15;
@@ -381,7 +270,6 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
     }
     if (l == 0 && !ok) flags[0] = 1;
       };
-#endif
   const int li = l & 15, lk = l >> 4;
   // one tile update (I, J) -= L[I, K] L[J, K]^T on the matrix cores (two
   // tiles at a time: independent MFMA chains); `on` masks the second one
@@ -423,9 +311,6 @@ __device__ __forceinline__ bool cholesky(double *lds, const double *__restrict__
     }
     __syncthreads();
     clk.tick(13);
-#ifdef GY
-    if (wv == 4) y_block(K);
-#endif
     if (K + 1 < T) {
       // look-ahead: wavefront 0 updates the next diagonal tile and factorises
       // it while the others update the rest of the trailing matrix
@@ -538,7 +423,11 @@ struct Rows {
 };
 
 // ------------------------------------------------------------------ kernel
-template <bool STAMP>
+// BOX: lb <= x <= ub with A = [I; -I] implicit (qpb_solve_box for 32 < n <= 128):
+// Ag = lb, bg = ub (n per QP, either may be NULL: absent bounds), m = 2n; the
+// rows of A are generated where they are loaded (D = A L^{-T} is formed as for
+// a dense A; nothing else reads A)
+template <bool STAMP, bool BOX = false>
 __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg, uint32_t *__restrict__ actg,
@@ -583,11 +472,11 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     const long long g = flags[1];
     if (g >= batch) break;
     const double *Hq = Hg + g * (long long)n * n;
-    const double *Aq = Ag + g * (long long)m * n;
+    const double *Aq = BOX ? Hq : Ag + g * (long long)m * n;
 
     // ------------------------------------------------------------ setup
     clk.tick(10);
-    const bool spd = cholesky(lds, Hq, fg + g * n, n, T, tid, clk);
+    const bool spd = cholesky(lds, Hq, n, T, tid, clk);
 #ifdef GRAM_ONLY_CHOL
     if (tid == 0) statg[g] = spd;
     continue;
@@ -602,14 +491,12 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     }
     clk.tick(0);
     // y = L^{-1} f on wavefront 0, into yb (permuted), before D is live
-#ifndef GY
     if (wv == 0) {
       double a0 = l < n ? fg[g * n + l] : 0.0, a1 = l + 64 < n ? fg[g * n + l + 64] : 0.0;
       solve_lower(Lp, nb, l, a0, a1);
       yb[pad(perm(l))] = a0;
       yb[pad(perm(l + 64))] = a1;
     }
-#endif
     // this lane's entries of A and b, all issued before the first use: one
     // memory round trip.  Loads are unconditional (masked lanes read a
     // clamped address): a guarded load becomes a branch with its own wait.
@@ -617,7 +504,23 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
     // overwrites in place.
     double E[RT][8][4];
     double bl[RT];
-    if (m > 0) {
+    if constexpr (BOX) {
+      // row r < n: x_r <= ub_r (a = e_r); row n + i: -x_i <= -lb_i (a = -e_i);
+      // an absent bound (NULL array, NaN) is +inf: the row is never violated
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const int rr = row[t], c0 = rr < n ? rr : rr - n;
+        const double sg = rr < n ? 1.0 : -1.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) E[t][k][r] = (rowok[t] && 16 * k + lk + 4 * r == c0) ? sg : 0.0;
+        const double *bnd = rr < n ? bg : Ag;
+        const double v = (rowok[t] && bnd) ? bnd[g * n + c0] : (rr < n ? kInf : -kInf);
+        const double bv = rr < n ? v : -v;
+        bl[t] = rowok[t] ? (bv == bv ? bv : kInf) : 0.0;
+      }
+    } else if (m > 0) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
 #pragma unroll
@@ -1131,10 +1034,10 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
 }  // namespace qpb
 
 // scratch: per workgroup (NB - QL) D_W rows beyond the LDS ones + the queue head
-extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
-                                         const double *b, double *x, double *lam, uint32_t *active,
-                                         int32_t *status, int32_t *iters, unsigned long long *sections,
-                                         hipStream_t stream) {
+template <bool BOX>
+static hipError_t launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                 const double *b, double *x, double *lam, uint32_t *active, int32_t *status,
+                                 int32_t *iters, unsigned long long *sections, hipStream_t stream) {
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
   int dev = 0, cus = 0;
@@ -1149,14 +1052,29 @@ extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, con
     int *queue = reinterpret_cast<int *>(static_cast<char *>(buf) + rows_bytes);
     hipError_t err = hipMemsetAsync(queue, 0, sizeof(int), stream);
     if (err != hipSuccess) return err;
-    if (sections)
-      hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<true>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
+    if constexpr (!BOX)  // the stamped diagnostic build exists for the dense form only
+      if (sections) {
+        hipLaunchKernelGGL((qpb::gram::gi_gram_kernel<true, BOX>), dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
                          f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
                          queue, static_cast<double *>(buf), sections);
-    else
-      hipLaunchKernelGGL(qpb::gram::gi_gram_kernel<false>, dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
+        return hipGetLastError();
+      }
+    hipLaunchKernelGGL((qpb::gram::gi_gram_kernel<false, BOX>), dim3((unsigned)grid), dim3(qpb::gram::NT), 0, stream, H,
                          f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,
                          queue, static_cast<double *>(buf), nullptr);
     return hipGetLastError();
   });
+}
+
+extern "C" hipError_t qpb_launch_gi_gram(const qpb_desc *d, const double *H, const double *f, const double *A,
+                                         const double *b, double *x, double *lam, uint32_t *active,
+                                         int32_t *status, int32_t *iters, unsigned long long *sections,
+                                         hipStream_t stream) {
+  return launch_gi_gram<false>(d, H, f, A, b, x, lam, active, status, iters, sections, stream);
+}
+// qpb_solve_box for 32 < n <= 128: lb, ub in A's and b's places (d->m == 2 d->n)
+extern "C" hipError_t qpb_launch_gi_gram_box(const qpb_desc *d, const double *H, const double *f, const double *lb,
+                                             const double *ub, double *x, double *lam, uint32_t *active,
+                                             int32_t *status, int32_t *iters, hipStream_t stream) {
+  return launch_gi_gram<true>(d, H, f, lb, ub, x, lam, active, status, iters, nullptr, stream);
 }
