@@ -85,7 +85,7 @@ void qpb_compat_init(unsigned n_dim, double admm_box_min, double admm_box_max)
 	 * matrix library (matrix_mult, matrix_invert, matrix_norm, the pools)
 	 * works at any N_DIM up to 65535, and so does this one.  Only the three
 	 * qp_solvers.h solvers run on the batched GPU replicas, which take
-	 * n <= QPB_MAX_N; they refuse a larger N_DIM with the reason (run_ref). */
+	 * n <= QPB_REF_MAX_N (1024); they refuse a larger N_DIM with the reason (run_ref). */
 	if (n_dim == 0 || n_dim > 0xFFFFu) {
 		fprintf(stderr, "kmalloc_init: N_DIM = %u is outside 1..65535 (the 16-bit dimension fields of "
 				"struct _matrix, matrix_type.h)\n", n_dim);
@@ -491,14 +491,14 @@ struct _matrix *quadratic_form_eval_grad(struct _quadratic_form *qf, struct _mat
 /* ------------------------------------------------------------- solvers */
 static struct _matrix *run_ref(int mode, struct _matrix *x0, unsigned iterations, struct _quadratic_form *qf)
 {
-	if (MATRIX_GET_ROW(qf->p) > QPB_MAX_N) {
+	if (MATRIX_GET_ROW(qf->p) > QPB_REF_MAX_N) {
 		fprintf(stderr,
 			"%s: N_DIM = %u: the qp_solvers.h solvers of this library run on the batched GPU replicas "
-			"(qpb_ref_solve), which take n <= %d (qpb.h QPB_MAX_N); the matrix_ops.h routines have no "
+			"(qpb_ref_solve), which take n <= %d (qpb.h QPB_REF_MAX_N); the matrix_ops.h routines have no "
 			"such limit\n",
 			mode == QPB_REF_GD ? "gradient_descent_with_line_search"
 					   : mode == QPB_REF_NEWTON ? "newton_method_with_line_search" : "admm",
-			(unsigned)MATRIX_GET_ROW(qf->p), QPB_MAX_N);
+			(unsigned)MATRIX_GET_ROW(qf->p), QPB_REF_MAX_N);
 		exit(EXIT_FAILURE); /* the reference exits on its fatal errors (qp_solvers.c:79-82) */
 	}
 	struct _matrix *x = matrix_alloc(Nx1);

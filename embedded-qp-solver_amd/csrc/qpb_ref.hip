@@ -35,16 +35,25 @@
 //   kept all four matrices in a global slice with 8 workgroups per CU: one
 //   dependent memory round trip per multiply-add, 128-156 ms for configs[3]'s
 //   Newton replicas (74 ms now).
-// The arithmetic is the same code in the same order in both layouts: only the
+//   128 < n <= 1024 (round 6: the compat layer's N_DIM above 128, SURVEY's
+//   16-bit dimension fields): 1024-thread workgroups, one thread per row as
+//   for n <= 64, the four matrices (P, the LU, W, V) in a 4 n^2 slice of global
+//   memory per workgroup and only the n-vectors in LDS; the pivot search
+//   reduces over the sixteen wavefronts through LDS.  The n <= 64 code runs
+//   unchanged on those addresses.
+// The arithmetic is the same code in the same order in every layout: only the
 // addresses, and the grouping of loads ahead of the stores, change.
 #include "qpb_common.h"
 #include "qpb.h"
 
 namespace qpb {
 
-constexpr int REF_MAXN = 128;
+constexpr int REF_MAXN = 1024;
 constexpr int REF_LDS_MAXN = 64;  // n above this: the one-matrix layout (X) below
+constexpr int REF_BIG_MAXN = 128;  // n above this: the global layout below
 constexpr int REF_BIG_NT = 128;
+constexpr int REF_HUGE_NT = 1024;  // 128 < n <= 1024: one thread per row, the matrices in global memory
+constexpr int REF_HUGE_WS_MATS = 4;  // P, the LU, W, V per workgroup
 constexpr int REF_WS_MATS = 2;  // big layout, per workgroup: the LU factors (row-major), V (column-major)
 constexpr int REF_MAX_WG_PER_CU = 8;
 __host__ __device__ constexpr int ref_ld(int n) { return n | 1; }
@@ -164,8 +173,8 @@ __device__ void ref_lu(RefShared &S, const Mat &M, int n) {
     if constexpr (NT > 64) {
       // the wave's max (fmin of -v over the DPP rows, then the four rows:
       // fmin / fmax drop a NaN as the strict `>` scan skips it), its lowest
-      // thread at the max, then the two waves' pairs through LDS with ONE
-      // barrier (wave 0 wins ties: lower rows; a NaN wave max loses)
+      // thread at the max, then the waves' pairs through LDS with ONE
+      // barrier (lower waves win ties: lower rows; a NaN wave max loses)
       double m = -row_min(-v);
       m = __builtin_fmax(__builtin_fmax(readlane_d(m, 0), readlane_d(m, 16)),
                          __builtin_fmax(readlane_d(m, 32), readlane_d(m, 48)));
@@ -176,9 +185,16 @@ __device__ void ref_lu(RefShared &S, const Mat &M, int n) {
         S.redi[w] = hit ? (tid & ~63) + __builtin_ctzll(hit) : 1 << 30;
       }
       __syncthreads();
-      const double m0 = S.red[0], m1 = S.red[1];
-      piv = __builtin_fmax(m0, m1);
-      pidx = (m1 > m0 || m0 != m0) ? S.redi[1] : S.redi[0];
+      piv = S.red[0];
+      pidx = S.redi[0];
+#pragma unroll
+      for (int w2 = 1; w2 < NT / 64; ++w2) {
+        const double mw = S.red[w2];
+        if (mw > piv || piv != piv) {
+          pidx = S.redi[w2];
+          piv = __builtin_fmax(piv, mw);
+        }
+      }
     } else {
       piv = v;
 #pragma unroll
@@ -205,7 +221,7 @@ __device__ void ref_lu(RefShared &S, const Mat &M, int n) {
       M(i, k) = tmp;
       // the row's update RC entries at a time: their loads first, then the
       // arithmetic and the stores (one LDS latency per RC entries)
-      if constexpr (NT > 64) {
+      if constexpr (NT == REF_BIG_NT) {
         // the big layout: RC-aligned chunks over the padded columns, no
         // branch anywhere (a branch per guarded load made every join wait
         // for all outstanding LDS reads): entries j <= k and j >= n are
@@ -245,18 +261,20 @@ __device__ void ref_lu(RefShared &S, const Mat &M, int n) {
           }
       }
     }
-    // NT > 64: the next step's pivot search reads only the thread's own row,
-    // and its barrier comes before anything reads another thread's row
-    if constexpr (NT <= 64) __syncthreads();
+    // the big layout: the next step's pivot search reads only the thread's
+    // own row, and its barrier comes before anything reads another thread's row
+    if constexpr (NT != REF_BIG_NT) __syncthreads();
   }
-  if constexpr (NT > 64) __syncthreads();
+  if constexpr (NT == REF_BIG_NT) __syncthreads();
 }
 
-// In-place explicit inverse (matrix_invert, matrix_ops.c:551-630), n <= 64:
-// S.M -> S.Vr.  Thread i: row i in the LU, column i in the solves.
+// In-place explicit inverse (matrix_invert, matrix_ops.c:551-630), n <= 64
+// (NT = 64, LDS) or 128 < n <= 1024 (NT = 1024, global): S.M -> S.Vr.
+// Thread i: row i in the LU, column i in the solves.
+template <int NT>
 __device__ void ref_invert_small(RefShared &S, int n) {
   const Mat M{S.M, n, 1};
-  ref_lu<64>(S, M, n);
+  ref_lu<NT>(S, M, n);
   // per-column solves (:594-619): thread i solves for column i; its w/v
   // vectors are column i of W/V, so V ends up as the inverse (:621-625)
   const int tid = threadIdx.x;
@@ -438,7 +456,7 @@ template <int NT>
 __device__ __forceinline__ void ref_carve(RefShared &S, double *sm, double *ws, int n, bool with_p) {
   const int nn2 = n * n;
   double *cur = sm;
-  if constexpr (NT > 64) {
+  if constexpr (NT == REF_BIG_NT) {
     S.ld = ref_ld(n);
     S.X = cur;
     cur += ref_npad(n) * S.ld;
@@ -446,6 +464,14 @@ __device__ __forceinline__ void ref_carve(RefShared &S, double *sm, double *ws, 
     cur += 2 * ref_npad(n);
     S.Mg = ws + (size_t)blockIdx.x * REF_WS_MATS * nn2;
     S.P = Mat{S.X, 1, S.ld};  // where P is loaded (column-major)
+  } else if constexpr (NT == REF_HUGE_NT) {
+    // the n <= 64 layout's matrices in the workgroup's global slice
+    double *gm = ws + (size_t)blockIdx.x * REF_HUGE_WS_MATS * nn2;
+    S.ld = n;
+    S.P = Mat{gm, n, 1};
+    S.M = gm + nn2;
+    S.W = gm + 2 * nn2;
+    S.Vr = gm + 3 * nn2;
   } else {
     S.ld = n;
     if (with_p) {
@@ -467,7 +493,7 @@ __device__ __forceinline__ void ref_carve(RefShared &S, double *sm, double *ws, 
   S.t2 = S.t1 + n;
   S.scal = S.t2 + 4 * n;  // q, u, z sit between t2 and the scalars
   S.red = S.scal + 8;
-  S.perm = reinterpret_cast<int *>(S.red + 2);
+  S.perm = reinterpret_cast<int *>(S.red + (NT / 64 > 2 ? NT / 64 : 2));  // one reduction slot per wave
   S.redi = S.perm + n;
 }
 
@@ -477,7 +503,7 @@ template <int NT>
 __device__ __forceinline__ void ref_load_m(RefShared &S, const double *Pq, int n, double diag) {
   const int tid = threadIdx.x;
   const int nn2 = n * n;
-  if constexpr (NT > 64) {
+  if constexpr (NT == REF_BIG_NT) {
     for (int e = tid; e < nn2; e += NT) {
       const int r = e / n, c = e - r * n;
       S.X[c * S.ld + r] = Pq[e];
@@ -487,7 +513,7 @@ __device__ __forceinline__ void ref_load_m(RefShared &S, const double *Pq, int n
   }
   __syncthreads();
   if (diag != 0.0) {  // R = P + rho I (qp_solvers.c:285-291)
-    double *mii = NT > 64 ? &S.X[tid * S.ld + tid] : &S.M[tid * n + tid];
+    double *mii = NT == REF_BIG_NT ? &S.X[tid * S.ld + tid] : &S.M[tid * n + tid];
     if (tid < n) *mii = *mii + diag;
     __syncthreads();
   }
@@ -506,8 +532,8 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
   double *u = q + n;
   double *z = u + n;
   const double *Pq = Pg + g * (long long)nn2;
-  // P row-major in LDS (n <= 64); for n > 64 it is loaded after the invert
-  if constexpr (NT <= 64) {
+  // P row-major (n <= 64: LDS; n > 128: global); for 64 < n <= 128 it is loaded after the invert
+  if constexpr (NT != REF_BIG_NT) {
     for (int e = tid; e < nn2; e += NT) S.P.p[e] = Pq[e];
   }
   if (tid < n) {
@@ -521,7 +547,7 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
     const double MIN_GRAD = 1e-1;  // MIN_GRAD_GRAD / MIN_GRAD_NEWTON (:14-15)
     if (mode == QPB_REF_NEWTON) {  // hessian_inv = invert(copy(P)) (:115-117)
       ref_load_m<NT>(S, Pq, n, 0.0);
-      if constexpr (NT > 64) {
+      if constexpr (NT == REF_BIG_NT) {
         ref_invert_big(S, n);
         // V to the global slice (column-major: coalesced row products), P into X
         double *Vg = S.Mg + nn2;
@@ -532,10 +558,10 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
         __syncthreads();
         S.V = Mat{Vg, 1, n};
       } else {
-        ref_invert_small(S, n);
+        ref_invert_small<NT>(S, n);
       }
     }
-    if constexpr (NT > 64) {
+    if constexpr (NT == REF_BIG_NT) {
       for (int e = tid; e < nn2; e += NT) {
         const int r = e / n, c = e - r * n;
         S.X[c * S.ld + r] = Pq[e];
@@ -568,10 +594,10 @@ __device__ void ref_solve_one(double *sm, double *ws, int mode, int n, long long
       u[tid] = 0.0;
     }
     ref_load_m<NT>(S, Pq, n, rho);  // R = P + rho I (:285-291)
-    if constexpr (NT > 64)
+    if constexpr (NT == REF_BIG_NT)
       ref_invert_big(S, n);  // R^{-1} in X (:292)
     else
-      ref_invert_small(S, n);
+      ref_invert_small<NT>(S, n);
     const double sq = __builtin_sqrt((double)n);
     // admm_update_x's right-hand side rho (z - u) - q (:146-159) is each
     // thread's own entry, so it is formed at the end of the previous
@@ -684,13 +710,13 @@ __global__ __launch_bounds__(NT) void ref_invert_kernel(int n, long long batch, 
     RefShared S;
     ref_carve<NT>(S, sm, ws, n, false);
     const double *Pq = Pg + g * (long long)nn2;
-    if constexpr (NT > 64) {
+    if constexpr (NT == REF_BIG_NT) {
       ref_load_m<NT>(S, Pq, n, 0.0);
       ref_invert_big(S, n);
     } else {
       for (int e = tid; e < nn2; e += NT) S.M[e] = Pq[e];
       __syncthreads();
-      ref_invert_small(S, n);
+      ref_invert_small<NT>(S, n);
     }
     double *Vq = Vg + g * (long long)nn2;
     for (int e = tid; e < nn2; e += NT) {
@@ -709,8 +735,29 @@ namespace {
 // (doubles), perm + 2 (ints)
 size_t ref_lds_bytes(int n, bool with_p) {
   const size_t nn2 = (size_t)n * n;
+  if (n > qpb::REF_BIG_MAXN)  // the matrices live in the workspace; 16 reduction slots
+    return sizeof(double) * (9 * (size_t)n + 8 + 16) + sizeof(int) * ((size_t)n + 16);
   const size_t mats = n <= qpb::REF_LDS_MAXN ? (with_p ? nn2 : 0) + 3 * nn2 : (size_t)qpb::ref_npad(n) * (qpb::ref_ld(n) + 2);
   return sizeof(double) * (mats + 9 * (size_t)n + 10) + sizeof(int) * ((size_t)n + 2);
+}
+// 128 < n <= 1024: one 1024-thread workgroup per CU at most, each with a
+// 4 n^2 slice of the cached workspace, the grid capped so that the slices
+// stay within 2 GiB (64 workgroups at n = 1024)
+hipError_t ref_huge_launch(long long batch, int n, hipStream_t stream,
+                           const std::function<void(unsigned grid, double *ws)> &launch) {
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const size_t slice = (size_t)qpb::REF_HUGE_WS_MATS * (size_t)n * n * sizeof(double);
+  long long cap = (long long)((2ull << 30) / slice);
+  if (cap < 1) cap = 1;
+  if (cap > cus) cap = cus;
+  const unsigned grid = (unsigned)(batch < cap ? batch : cap);
+  return qpb_with_workspace(stream, (size_t)grid * slice, [&](void *p) {
+    launch(grid, static_cast<double *>(p));
+    return hipGetLastError();
+  });
 }
 // n > 64: as many workgroups per CU as their LDS allows (one at n = 128, at
 // most REF_MAX_WG_PER_CU) walk the batch, each with its 2 n^2 slice of the
@@ -752,6 +799,14 @@ extern "C" hipError_t qpb_launch_ref_invert(int n, long long batch, const double
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(qpb::ref_invert_kernel<64>, dim3((unsigned)batch), dim3(64), lds, stream, n, batch, P, Pinv,
                        nullptr);
+  } else if (n > qpb::REF_BIG_MAXN) {
+    hipError_t e = allow_lds(&qpb::ref_invert_kernel<qpb::REF_HUGE_NT>, lds);
+    if (e == hipSuccess)
+      e = ref_huge_launch(batch, n, stream, [&](unsigned grid, double *ws) {
+        hipLaunchKernelGGL(qpb::ref_invert_kernel<qpb::REF_HUGE_NT>, dim3(grid), dim3(qpb::REF_HUGE_NT), lds, stream,
+                           n, batch, P, Pinv, ws);
+      });
+    if (e != hipSuccess) return e;
   } else {
     hipError_t e = allow_lds(&qpb::ref_invert_kernel<128>, lds);
     if (e == hipSuccess)
@@ -781,6 +836,15 @@ extern "C" hipError_t qpb_launch_ref(const qpb_ref_desc *d, const double *P, con
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(qpb::ref_kernel<64>, dim3((unsigned)d->batch), dim3(64), lds, stream, d->mode, n,
                        (long long)d->batch, d->iterations, d->box_min, d->box_max, P, q, x0, x, iters, nullptr);
+  } else if (n > qpb::REF_BIG_MAXN) {
+    hipError_t e = allow_lds(&qpb::ref_kernel<qpb::REF_HUGE_NT>, lds);
+    if (e == hipSuccess)
+      e = ref_huge_launch(d->batch, n, stream, [&](unsigned grid, double *ws) {
+        hipLaunchKernelGGL(qpb::ref_kernel<qpb::REF_HUGE_NT>, dim3(grid), dim3(qpb::REF_HUGE_NT), lds, stream,
+                           d->mode, n, (long long)d->batch, d->iterations, d->box_min, d->box_max, P, q, x0, x, iters,
+                           ws);
+      });
+    if (e != hipSuccess) return e;
   } else {
     hipError_t e = allow_lds(&qpb::ref_kernel<128>, lds);
     if (e == hipSuccess)

