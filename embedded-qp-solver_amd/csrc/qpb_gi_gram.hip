@@ -431,11 +431,21 @@ __device__ __forceinline__ void solve_upper(const double *Lp, int nb, int l, dou
 __device__ __forceinline__ void solve_lower_blk(const double *Lp, const double *LIb, double *v, int T, int lane) {
   const int i = lane & 15, g4 = lane >> 4;
   for (int K = 0; K < T; ++K) {
+    // this lane's quarter of the finished entries (4K of them), every read
+    // issued before the first FMA (one LDS round trip per block, not per term)
+    constexpr int MM = 4 * (NB / 16 - 1);
+    double lv[MM], vv[MM];
+#pragma unroll
+    for (int mm = 0; mm < MM; ++mm) {
+      const int j = mm < 4 * K ? 4 * mm + g4 : 0;
+      lv[mm] = Lp[tri(16 * K + i, j)];
+      vv[mm] = v[pad(perm(j))];
+    }
     double p0 = 0.0, p1 = 0.0;
-    for (int mm = 0; mm < 4 * K; mm += 2) {
-      const int j0 = 4 * mm + g4, j1 = j0 + 4;
-      p0 = __builtin_fma(Lp[tri(16 * K + i, j0)], v[pad(perm(j0))], p0);
-      p1 = __builtin_fma(Lp[tri(16 * K + i, j1)], v[pad(perm(j1))], p1);
+#pragma unroll
+    for (int mm = 0; mm < MM; mm += 2) {
+      p0 = mm < 4 * K ? __builtin_fma(lv[mm], vv[mm], p0) : p0;
+      p1 = mm + 1 < 4 * K ? __builtin_fma(lv[mm + 1], vv[mm + 1], p1) : p1;
     }
     const double acc = v[pad(perm(16 * K + i))] - group_sum(p0 + p1);
     dpp_ready(acc);
@@ -454,12 +464,20 @@ __device__ __forceinline__ void solve_lower_blk(const double *Lp, const double *
 __device__ __forceinline__ void solve_upper_blk(const double *Lp, const double *LIb, double *v, int T, int lane) {
   const int i = lane & 15, g4 = lane >> 4;
   for (int K = T - 1; K >= 0; --K) {
+    constexpr int MM = 4 * (NB / 16 - 1);
+    const int cnt = 4 * (T - 1 - K), j00 = 16 * (K + 1);
+    double lv[MM], vv[MM];
+#pragma unroll
+    for (int mm = 0; mm < MM; ++mm) {
+      const int j = mm < cnt ? j00 + 4 * mm + g4 : 16 * K + i;  // in range either way
+      lv[mm] = Lp[tri(j, 16 * K + i)];
+      vv[mm] = v[pad(perm(j))];
+    }
     double p0 = 0.0, p1 = 0.0;
-    const int j00 = 16 * (K + 1);
-    for (int mm = 0; mm < 4 * (T - 1 - K); mm += 2) {
-      const int j0 = j00 + 4 * mm + g4, j1 = j0 + 4;
-      p0 = __builtin_fma(Lp[tri(j0, 16 * K + i)], v[pad(perm(j0))], p0);
-      p1 = __builtin_fma(Lp[tri(j1, 16 * K + i)], v[pad(perm(j1))], p1);
+#pragma unroll
+    for (int mm = 0; mm < MM; mm += 2) {
+      p0 = mm < cnt ? __builtin_fma(lv[mm], vv[mm], p0) : p0;
+      p1 = mm + 1 < cnt ? __builtin_fma(lv[mm + 1], vv[mm + 1], p1) : p1;
     }
     const double acc = v[pad(perm(16 * K + i))] - group_sum(p0 + p1);
     dpp_ready(acc);
