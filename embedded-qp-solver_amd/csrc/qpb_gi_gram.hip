@@ -87,11 +87,7 @@ constexpr int R_KEY = 0;    // per-wave selection keys (NWV)
 constexpr int R_T1 = 8;     // per-wave (ratio min, argmin position) pairs (2 NWV)
 constexpr int R_ND2 = 24;   // per-wave partial |w|^2 (NWV)
 constexpr double kDepTol = 1e-24;
-#ifdef GRAM_BLK
-constexpr long long SCRATCH = LP + (long long)(NB - QL) * NB + 8 * LIT;  // doubles per workgroup (+ the tile inverses)
-#else
 constexpr long long SCRATCH = LP + (long long)(NB - QL) * NB;  // doubles per workgroup
-#endif
 
 using d4 = __attribute__((__vector_size__(4 * sizeof(double)))) double;
 
@@ -419,81 +415,6 @@ __device__ __forceinline__ void solve_upper(const double *Lp, int nb, int l, dou
   a1 *= id1;
 }
 
-#ifdef GRAM_BLK
-// Blocked triangular solves on one wavefront with the diagonal tiles'
-// inverses LI (LI[K][j][i] = (L_KK^{-1})[j][i], row stride LIS): 16-row
-// blocks in T steps instead of n readlane steps.  Lane (g4, i): the block's
-// off-diagonal sum over its quarter of the finished entries, the quarters
-// added (group_sum), then the tile inverse applied with the sum read from
-// lane j of the same DPP row by the FMAs.  v: the permuted vector in LDS
-// (yb), overwritten block by block with the solution.
-// L y = v (forward):   y_K = Linv_K (v_K - sum_{j < 16K} L[16K + i][j] y_j)
-__device__ __forceinline__ void solve_lower_blk(const double *Lp, const double *LIb, double *v, int T, int lane) {
-  const int i = lane & 15, g4 = lane >> 4;
-  for (int K = 0; K < T; ++K) {
-    // this lane's quarter of the finished entries (4K of them), every read
-    // issued before the first FMA (one LDS round trip per block, not per term)
-    constexpr int MM = 4 * (NB / 16 - 1);
-    double lv[MM], vv[MM];
-#pragma unroll
-    for (int mm = 0; mm < MM; ++mm) {
-      const int j = mm < 4 * K ? 4 * mm + g4 : 0;
-      lv[mm] = Lp[tri(16 * K + i, j)];
-      vv[mm] = v[pad(perm(j))];
-    }
-    double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < MM; mm += 2) {
-      p0 = mm < 4 * K ? __builtin_fma(lv[mm], vv[mm], p0) : p0;
-      p1 = mm + 1 < 4 * K ? __builtin_fma(lv[mm + 1], vv[mm + 1], p1) : p1;
-    }
-    const double acc = v[pad(perm(16 * K + i))] - group_sum(p0 + p1);
-    dpp_ready(acc);
-    double y0 = 0.0, y1 = 0.0;
-    unroll<16>([&](auto Jc) {
-      constexpr int jj = Jc;
-      if constexpr (jj % 2 == 0) fmac_bc<jj>(y0, acc, LIb[K * LIT + i * LIS + jj]);
-      if constexpr (jj % 2 == 1) fmac_bc<jj>(y1, acc, LIb[K * LIT + i * LIS + jj]);
-    });
-    wave_lds_sync();
-    if (g4 == 0) v[pad(perm(16 * K + i))] = y0 + y1;
-    wave_lds_sync();
-  }
-}
-// L^T x = v (backward): x_K = Linv_K^T (v_K - sum_{j >= 16(K+1)} L[j][16K + i] x_j)
-__device__ __forceinline__ void solve_upper_blk(const double *Lp, const double *LIb, double *v, int T, int lane) {
-  const int i = lane & 15, g4 = lane >> 4;
-  for (int K = T - 1; K >= 0; --K) {
-    constexpr int MM = 4 * (NB / 16 - 1);
-    const int cnt = 4 * (T - 1 - K), j00 = 16 * (K + 1);
-    double lv[MM], vv[MM];
-#pragma unroll
-    for (int mm = 0; mm < MM; ++mm) {
-      const int j = mm < cnt ? j00 + 4 * mm + g4 : 16 * K + i;  // in range either way
-      lv[mm] = Lp[tri(j, 16 * K + i)];
-      vv[mm] = v[pad(perm(j))];
-    }
-    double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-    for (int mm = 0; mm < MM; mm += 2) {
-      p0 = mm < cnt ? __builtin_fma(lv[mm], vv[mm], p0) : p0;
-      p1 = mm + 1 < cnt ? __builtin_fma(lv[mm + 1], vv[mm + 1], p1) : p1;
-    }
-    const double acc = v[pad(perm(16 * K + i))] - group_sum(p0 + p1);
-    dpp_ready(acc);
-    double x0 = 0.0, x1 = 0.0;
-    unroll<16>([&](auto Jc) {
-      constexpr int jj = Jc;
-      if constexpr (jj % 2 == 0) fmac_bc<jj>(x0, acc, LIb[K * LIT + jj * LIS + i]);
-      if constexpr (jj % 2 == 1) fmac_bc<jj>(x1, acc, LIb[K * LIT + jj * LIS + i]);
-    });
-    wave_lds_sync();
-    if (g4 == 0) v[pad(perm(16 * K + i))] = x0 + x1;
-    wave_lds_sync();
-  }
-}
-#endif
-
 // ------------------------------------------------------- Q1 row storage
 struct Rows {
   double *lds;  // rows 0..QL-1, stride QS
@@ -568,24 +489,13 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
       const int e = tid + NT * u;
       if (e < tri(nb, 0)) Lgl[e] = Lp[e];
     }
-#ifdef GRAM_BLK
-    // the diagonal tiles' inverses too (the loop's Q1 rows overwrite them)
-    for (int e = tid; e < T * LIT; e += NT) Lgl[LP + (NB - QL) * NB + e] = lds[OFF_ROWS + e];
-#endif
     clk.tick(0);
     // y = L^{-1} f on wavefront 0, into yb (permuted), before D is live
     if (wv == 0) {
       double a0 = l < n ? fg[g * n + l] : 0.0, a1 = l + 64 < n ? fg[g * n + l + 64] : 0.0;
-#ifdef GRAM_BLK
-      yb[pad(perm(l))] = a0;
-      yb[pad(perm(l + 64))] = a1;
-      wave_lds_sync();
-      solve_lower_blk(Lp, lds + OFF_ROWS, yb, T, l);
-#else
       solve_lower(Lp, nb, l, a0, a1);
       yb[pad(perm(l))] = a0;
       yb[pad(perm(l + 64))] = a1;
-#endif
     }
     // this lane's entries of A and b, all issued before the first use: one
     // memory round trip.  Loads are unconditional (masked lanes read a
@@ -1096,22 +1006,11 @@ __global__ __launch_bounds__(NT, 1) void gi_gram_kernel(
           if (e < ne) Lp[e] = lv[u];
         }
       }
-#ifdef GRAM_BLK
-      for (int e = tid; e < T * LIT; e += NT) lds[OFF_ROWS + e] = Lgl[LP + (NB - QL) * NB + e];
-#endif
       __syncthreads();
       clk.tick(8);
       if (wv == 0) {
-#ifdef GRAM_BLK
-        yb[pad(perm(l))] = -yb[pad(perm(l))];
-        yb[pad(perm(l + 64))] = -yb[pad(perm(l + 64))];
-        wave_lds_sync();
-        solve_upper_blk(Lp, lds + OFF_ROWS, yb, T, l);
-        double x0 = yb[pad(perm(l))], x1 = yb[pad(perm(l + 64))];
-#else
         double x0 = -yb[pad(perm(l))], x1 = -yb[pad(perm(l + 64))];
         solve_upper(Lp, nb, l, x0, x1);
-#endif
         if (l < n) xg[g * n + l] = x0;
         if (l + 64 < n) xg[g * n + l + 64] = x1;
         const bool bad = (l < n && !(__builtin_fabs(x0) < kInf)) || (l + 64 < n && !(__builtin_fabs(x1) < kInf));
