@@ -730,65 +730,14 @@ __device__ __forceinline__ void gi_group(
   clk.flush(dbg);
 }
 
-// The dynamic tail of a large launch (tick != nullptr).  The hardware hands
-// workgroup i to XCD i mod 8, so every XCD solves the same number of groups,
-// and the XCDs do not run at the same rate: at 1 M QPs the first finishes
-// 70-100 us before the last (tools/wave_timeline.py).  Workgroups below
-// `gstat` solve group blockIdx.x as before; the groups from gstat on are
-// split into eight ranges of `share`, one per XCD, which the workgroups past
-// gstat claim through eight device-scope counters (one 128-B line each,
-// zeroed before the launch): their own XCD's range first, then, once it is
-// used up, whichever range still has groups.  The tail holds more workgroups
-// than groups, so a fast XCD's surplus workgroups take the slow XCDs' groups
-// and the rest find every range used up and leave.  Every group is claimed
-// exactly once: a claim is a fetch-add under the range's size; a failed one
-// leaves its range used up for good, so the search ends after at most nine
-// rounds with a group or with every range used up.  Wave-uniform throughout.
-__device__ __forceinline__ long long claim_tail_group(int *__restrict__ tick, long long gstat, int share,
-                                                     long long groups) {
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  xcc &= 7u;
-  const int lane = threadIdx.x & 63;
-  // groups in range y (the last ranges may be short or empty)
-  auto size_of = [&](int y) {
-    const long long left = groups - gstat - (long long)y * share;
-    return (int)(left < 0 ? 0 : left < share ? left : share);
-  };
-  int t = 0;
-  if (lane == 0) t = __hip_atomic_fetch_add(&tick[32 * xcc], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __builtin_amdgcn_readfirstlane(t);
-  if (t < size_of((int)xcc)) return gstat + (long long)xcc * share + t;
-  for (int round = 0; round < 9; ++round) {
-    // lanes 0..7 look at the ranges in the order xcc+1, xcc+2, ...
-    const int y = (int)((xcc + 1u + (unsigned)lane) & 7u);
-    bool room = false;
-    if (lane < 8) room = __hip_atomic_load(&tick[32 * y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < size_of(y);
-    const unsigned long long any = __ballot(room);
-    if (!any) return -1;
-    const int ys = (int)((xcc + 1u + (unsigned)__builtin_ctzll(any)) & 7u);
-    int ts = 0;
-    if (lane == 0) ts = __hip_atomic_fetch_add(&tick[32 * ys], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ts = __builtin_amdgcn_readfirstlane(ts);
-    if (ts < size_of(ys)) return gstat + (long long)ys * share + ts;
-  }
-  return -1;
-}
-
 template <int MR, bool N16, bool FULL, bool STAMP = false, int OCC = 2>
 __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
     const double *__restrict__ Hg, const double *__restrict__ fg, const double *__restrict__ Ag,
     const double *__restrict__ bg, double *__restrict__ xg, double *__restrict__ lamg,
     uint32_t *__restrict__ actg, int32_t *__restrict__ statg, int32_t *__restrict__ itg, int n, int m,
     long long batch, int max_iter, double feas_tol, int flags = 0,
-    unsigned long long *__restrict__ dbg = nullptr, int *__restrict__ tick = nullptr, long long gstat = 0,
-    int share = 0) {
+    unsigned long long *__restrict__ dbg = nullptr) {
   __shared__ double lds[QPB * SLOT];
-  long long grp = blockIdx.x;
-  if (tick && grp >= gstat) {
-    grp = claim_tail_group(tick, gstat, share, (batch + QPB - 1) / QPB);
-    if (grp < 0) return;
-  }
 #ifdef QPB_WAVE_TRACE
   // diagnostic build only (tools/wave_timeline.py): each wave's start and end
   // on the 100 MHz real-time and the shader clocks, and where it ran
@@ -800,9 +749,9 @@ __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
 #endif
   gi_group<MR, N16, FULL, STAMP>(lds, Hg, fg, Ag, bg, xg, lamg, actg, statg, itg, n, m, batch, max_iter, feas_tol,
 #ifdef QPB_WAVE_TRACE
-                                 flags, dbg, grp);
+                                 flags, dbg, blockIdx.x);
 #else
-                                 flags, STAMP ? dbg : nullptr, grp);
+                                 flags, STAMP ? dbg : nullptr, blockIdx.x);
 #endif
 #ifdef QPB_WAVE_TRACE
 #if QPB_WAVE_TRACE == 2
@@ -823,51 +772,28 @@ __global__ __launch_bounds__(64, OCC) void gi_dense_kernel(
 }  // namespace qpb
 
 // launcher used by qpb_api.hip
-#ifndef QPB_TAIL_MIN_GROUPS
-#define QPB_TAIL_MIN_GROUPS 65536  // the dynamic tail from 262 144 QPs on
-#endif
-#ifndef QPB_TAIL_DIV
-#define QPB_TAIL_DIV 8  // 1/8 of the groups in the tail
-#endif
-#ifndef QPB_TAIL_EXTRA
-#define QPB_TAIL_EXTRA 2  // tail workgroups: its groups + 1/2 of them
-#endif
 extern "C" hipError_t qpb_launch_gi(const qpb_desc *d, const double *H, const double *f, const double *A,
                                     const double *b, double *x, double *lam, uint32_t *active,
                                     int32_t *status, int32_t *iters, hipStream_t stream) {
   const long long blocks = (d->batch + qpb::QPB - 1) / qpb::QPB;
   const int max_iter = d->max_iter > 0 ? d->max_iter : 4 * (d->n + d->m) + 8;
   const double tol = d->feas_tol > 0 ? d->feas_tol : 1e-10;
-  auto launch = [&](long long grid, int *tick, long long gstat, int share) {
-#define QPB_GI_LAUNCH(MR, N16, FULL)                                                                                   \
-  hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL, false, 3>), dim3((unsigned)grid), dim3(64), 0, stream, H, f, \
-                     A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol, d->flags,     \
-                     nullptr, tick, gstat, share)
-    const bool n16 = d->n == 16;
-    if (d->m <= 16) {
-      if (n16 && d->m == 16) QPB_GI_LAUNCH(1, true, true);
-      else if (n16) QPB_GI_LAUNCH(1, true, false);
-      else QPB_GI_LAUNCH(1, false, false);
-    } else {
-      if (n16 && d->m == 32) QPB_GI_LAUNCH(2, true, true);  // 3 waves per SIMD (VGPRs and LDS)
-      else if (n16) QPB_GI_LAUNCH(2, true, false);
-      else QPB_GI_LAUNCH(2, false, false);
-    }
+#define QPB_GI_LAUNCH(MR, N16, FULL)                                                                               \
+  hipLaunchKernelGGL((qpb::gi_dense_kernel<MR, N16, FULL, false, 3>), dim3((unsigned)blocks), dim3(64), 0, stream, \
+                     H, f, A, b, x, lam, active, status, iters, d->n, d->m, (long long)d->batch, max_iter, tol,    \
+                     d->flags)
+  const bool n16 = d->n == 16;
+  if (d->m <= 16) {
+    if (n16 && d->m == 16) QPB_GI_LAUNCH(1, true, true);
+    else if (n16) QPB_GI_LAUNCH(1, true, false);
+    else QPB_GI_LAUNCH(1, false, false);
+  } else {
+    if (n16 && d->m == 32) QPB_GI_LAUNCH(2, true, true);  // 3 waves per SIMD (VGPRs and LDS)
+    else if (n16) QPB_GI_LAUNCH(2, true, false);
+    else QPB_GI_LAUNCH(2, false, false);
+  }
 #undef QPB_GI_LAUNCH
-    return hipGetLastError();
-  };
-  if (blocks < QPB_TAIL_MIN_GROUPS) return launch(blocks, nullptr, 0, 0);
-  // the dynamic tail (claim_tail_group): eight ranges of `share` groups, its
-  // counters in the stream's cached workspace, zeroed on the stream first
-  const long long share = blocks / QPB_TAIL_DIV / 8;
-  const long long gstat = blocks - 8 * share;
-  const long long grid = blocks + 8 * share / QPB_TAIL_EXTRA;
-  constexpr size_t kTickBytes = 8 * 32 * sizeof(int);
-  return qpb_with_workspace(stream, kTickBytes, [&](void *p) {
-    int *tick = static_cast<int *>(p);
-    const hipError_t e = hipMemsetAsync(tick, 0, kTickBytes, stream);
-    return e != hipSuccess ? e : launch(grid, tick, gstat, (int)share);
-  });
+  return hipGetLastError();
 }
 
 // diagnostic: per-section wave ticks of the n=16, 16<m<=32 kernel (sections[256][20])
