@@ -286,6 +286,13 @@ def main():
                     help="after the timed steps, the same K batches alternating over this many HIP streams "
                          "(a serving loop: one batch's drain overlaps the next one's ramp-up), reported "
                          "beside the line's single-stream value (0 or 1: skip)")
+    ap.add_argument("--settle-seconds", type=float, default=0.1,
+                    help="before the warmup steps, back-to-back solves of the same batch for about this long: "
+                         "after the CPU leg (or process start) the GPU is idle, and its first ~30 launches run "
+                         "up to 10 %% slower while its clocks ramp (tools/warm_state.py); reported (0: skip)")
+    ap.add_argument("--sustain-seconds", type=float, default=6.0,
+                    help="after the timed steps, back-to-back solves of the same batch for about this long "
+                         "(clock and thermal steady state), reported beside the line's value (0: skip)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -360,19 +367,36 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
+    # settle: the GPU out of its idle clocks before the warmup steps (every
+    # rank, the same span, launch groups of 5 with a sync between groups)
+    settle = None
+    if args.settle_seconds > 0:
+        barrier()
+        tw, kw = time.perf_counter(), 0
+        while time.perf_counter() - tw < args.settle_seconds:
+            for _ in range(5):
+                qpb.solve(H, f, A, b, out=sol, stream=stream)
+            kw += 5
+            torch.cuda.synchronize()
+        settle = {"seconds": time.perf_counter() - tw, "launches": kw,
+                  "what": "the line's solve back to back before the warmup steps: the GPU's first ~30 "
+                          "launches after idle run up to 10 % slower while its clocks ramp "
+                          "(tools/warm_state.py, profiles/r06/warm)"}
     for _ in range(args.warmup):
         qpb.solve(H, f, A, b, out=sol, stream=stream)
-    # HIP events on the stream the kernel is launched on
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the stream the kernel is launched on, one pair around the
+    # K launches (a pair around every launch slowed them by ~0.4 %,
+    # tools/event_overhead.py): the average launch duration, gaps included
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(args.steps):
-        evs[k][0].record(stream)
         qpb.solve(H, f, A, b, out=sol, stream=stream)
-        evs[k][1].record(stream)
+    ev1.record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(e) for a, e in evs) / args.steps
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     local_step_ms = elapsed / args.steps * 1e3
     elapsed = max_over_ranks(elapsed, device)
     if dist_info is not None:
@@ -427,6 +451,30 @@ def main():
                      "what": "the same K steps alternating over S HIP streams: a batch's drain (its last "
                              "waves finishing) overlaps the next batch's ramp-up (every wave slot loading)"}
         del psols
+
+    # sustained leg, outside the timed steps: the same solve back to back for
+    # about --sustain-seconds (launched 20 at a time, the host checking the
+    # clock between groups), barrier + max over ranks as above
+    sustained = None
+    if args.sustain_seconds > 0:
+        barrier()
+        ts = time.perf_counter()
+        ks = 0
+        while True:
+            for _ in range(20):
+                qpb.solve(H, f, A, b, out=sol, stream=stream)
+            ks += 20
+            torch.cuda.synchronize()
+            done = time.perf_counter() - ts >= args.sustain_seconds
+            if world > 1:  # every rank stops after the same number of groups (all past the span)
+                done = max_over_ranks(0.0 if done else 1.0, device) == 0.0
+            if done:
+                break
+        barrier()
+        sel = max_over_ranks(time.perf_counter() - ts, device)
+        sustained = {"seconds": sel, "steps": ks, "value": total_B * ks / sel, "ms_per_step": sel / ks * 1e3,
+                     "what": "the line's solve back to back for the whole span (launch groups of 20, a host "
+                             "sync between groups): the rate once clocks and temperature have settled"}
 
     st = sol.status.cpu()
     it = sol.iters.cpu().double()
@@ -507,6 +555,8 @@ def main():
     value = total_qps / elapsed
     if pipelined:
         pipelined["gain"] = pipelined["value"] / value - 1.0
+    if sustained:
+        sustained["ratio_to_value"] = sustained["value"] / value
     bpq = bytes_per_qp(n, m)
     achieved = B * bpq / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n, m, B, args.family, qpb.version())
@@ -548,6 +598,8 @@ def main():
             "gather": gather,
             "dense_family": dense,
             "pipelined": pipelined,
+            "settle": settle,
+            "sustained": sustained,
             "distributed": dist_info,
             "library": qpb.version(),
         }

@@ -75,7 +75,7 @@ def test_bench_gpus_2_runs_two_ranks(qpb):
     the self-describing `distributed` block."""
     env = dict(os.environ, QPB_DIST_BACKEND="gloo")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--global-batch", "8192",
-           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--gather"]
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--gather", "--sustain-seconds", "0.5"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -99,6 +99,9 @@ def test_bench_gpus_2_runs_two_ranks(qpb):
     # the pipelined leg (two streams per rank, max over ranks) gives the same answers
     pl = line["pipelined"]
     assert pl["streams"] == 2 and pl["answers_equal"] is True and pl["value"] > 0.0
+    # the sustained leg: both ranks stop after the same launch groups, past the span
+    su = line["sustained"]
+    assert su["steps"] >= 20 and su["steps"] % 20 == 0 and su["seconds"] >= 0.5 and su["value"] > 0.0
 
 
 def _rccl_worker(rank, port, total, out_dir):

@@ -27,6 +27,17 @@ for r in stats:
         res["min_ns"] = float(r["MinNs"])
         res["max_ns"] = float(r["MaxNs"])
         res["pct_of_gpu_time"] = float(r["Percentage"])
+# the timed steps alone: the trace command launches nothing of this kernel
+# after them, so they are its last `steps` dispatches (the average above also
+# holds the first launches after idle, slow while the clocks ramp, and the
+# settle and warmup launches)
+kt = rows(os.path.join(out_dir, "trace", "run_kernel_trace.csv"))
+kd = [(float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) for r in kt if KERNEL in r.get("Kernel_Name", "")]
+steps = int(os.environ.get("STEPS", 50))
+if len(kd) >= steps:
+    res["timed_steps"] = steps
+    res["timed_avg_ns"] = sum(kd[-steps:]) / steps
+    res["first_launch_ns"] = kd[0]
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     vals = [float(r["Counter_Value"]) for r in rows(os.path.join(out_dir, f"pmc_{c}", "run_counter_collection.csv"))
             if KERNEL in r["Kernel_Name"]]
