@@ -20,9 +20,21 @@ import bench  # noqa: E402
 qpb = None  # imported in main(), after the forked CPU leg (nothing before it touches the GPU)
 
 
+def settle(fn, seconds=0.05):
+    """fn back to back for about `seconds` (groups of 5, a sync between): the
+    GPU's clocks ramp for its first launches after idle (the
+    CPU leg before the first row leaves the GPU idle for ~10 s)"""
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+
+
 def t_kernel(fn, reps=5):
     s = torch.cuda.current_stream()
-    fn()
+    settle(fn)  # the clocks out of their idle state first (DESIGN.md §4)
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

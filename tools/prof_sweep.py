@@ -16,10 +16,20 @@ import bench  # noqa: E402
 import qpb  # noqa: E402
 
 
+def settle(fn, seconds=0.05):
+    """fn back to back for about `seconds` (groups of 5, a sync between): the
+    GPU's clocks ramp for its first launches after idle"""
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+
+
 def t_kernel(fn, reps=15):
     s = torch.cuda.current_stream()
-    for _ in range(3):
-        fn()
+    settle(fn)
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
