@@ -265,3 +265,31 @@ def test_huge_layout_grid_reuse_bitwise(qpb):
     inv = qpb.matrix_invert(torch.from_numpy(P).cuda()).cpu().numpy()
     for i in range(300):
         assert np.array_equal(inv[i], rc.invert(P[i].copy())), i
+
+
+def test_huge_layout_max_n_bitwise(qpb):
+    """The largest size the replicas take, n = QPB_REF_MAX_N = 1024 (one
+    1024-thread workgroup, one thread per row, 4 n^2 = 32 MiB of workspace):
+    matrix_invert, Newton (10 iterations) and GD (20) on one QP bitwise
+    against the compiled reference at N_DIM = 1024.  The QP comes from numpy
+    (P = B^T B / (1e3 n) symmetrised, the distributions of matirx_random_pos_def,
+    matrix_ops.c:699-734): the reference's own generator needs ~10 s of CPU
+    at this size and bitwise parity only needs the same input bits on both sides.
+    (ADMM is left to n <= 300: one 1e4-iteration solve is ~1 min of CPU here.)"""
+    import refc
+    n = 1024
+    if not refc.available(n, "1e12"):
+        pytest.skip("oracle/_ref not built")
+    rc = refc.RefC(n, "1e12")
+    rng = np.random.default_rng(1024)
+    Bm = rng.uniform(-1e3, 1e3, (n, n))
+    P = Bm.T @ Bm / (1e3 * n)
+    P = ((P + P.T) * 0.5)[None]
+    q = rng.uniform(-1e3, 1e3, (1, n))
+    x0 = rng.uniform(-1e3, 1e3, (1, n))
+    inv = qpb.matrix_invert(torch.from_numpy(P).cuda()).cpu().numpy()
+    assert np.array_equal(inv[0], rc.invert(P[0].copy()))
+    x, _ = _run(qpb, qpb.REF_NEWTON, P, q, x0, 10)
+    assert np.array_equal(x, rc.newton(P, q, x0, 10))
+    x, _ = _run(qpb, qpb.REF_GD, P, q, x0, 20)
+    assert np.array_equal(x, rc.gd(P, q, x0, 20))
