@@ -396,4 +396,4 @@ extern "C" const char *qpb_last_error(void) { return g_err; }
 
 // the hot kernel revision is part of the string: profiles/pmc_traffic.json is
 // only trusted for the revision it was measured on (bench.py)
-extern "C" const char *qpb_version(void) { return "qpb 0.12 (gfx950; gi_dense v11.5: dual steepest-edge select -s/|D[r,q:]| with a nonzero key floor, dependency scale clamped to FLT_MAX, setup slacks from the sweep's DPP-read f, output stores under the A-row loads, DPP-fused slack product and Householder update, Householder product as u + alpha D[:,q], exact ratio step, one-trip loads and x gather, 3 waves/SIMD and 12 per CU (12,608 B of LDS per wave: the exchange row in R's column 0, Givens parameters in registers), built without machine LICM; gi_box v2.2: lb <= x <= ub, A implicit, dual steepest-edge select with a nonzero key floor, DPP-fused slack and Householder products, one-pass R column shift, 12 waves per CU; gi_wave v6.6 (+ BOX, n <= 32; absent bounds as +inf slacks): dual steepest-edge select with a nonzero key floor, ratio reduction only when a partial step is possible, active A rows for x gathered 16 at a time, DPP-fused sweep, slack product, Householder update and back substitution (no LDS vector reads), Householder product as u + alpha D[:,q], odd-stride R with the exchange row in its column 0 (12 waves per CU), one-trip A gather for x, split setup sweep, 3 waves/SIMD; gi_gram v4.5 (+ BOX, n <= 128: qpb_solve_box with A generated in place) n<=128 on fp64 MFMA, no next-QP prefetch, lane ids opaque per iteration (2 VGPR spills instead of 29), active set as Q1 rows and Z = R^{-1} (parallel passes only), |u|^2 published with the key, broadcast row products, conflict-free diagonal-tile inverses, one-trip loads, cached workspace launched under its lock; ref v6: n <= 1024 (above 128: 1024-thread workgroups, the matrices in a global workspace slice), 64 < n <= 128 one LDS matrix per workgroup (LU, W / V, P in turn), LU rows staged for the solves, branch-free chunked sums)"; }
+extern "C" const char *qpb_version(void) { return "qpb 0.12 (gfx950; gi_dense v11.5: dual steepest-edge select -s/|D[r,q:]| with a nonzero key floor, dependency scale clamped to FLT_MAX, setup slacks from the sweep's DPP-read f, output stores under the A-row loads, DPP-fused slack product and Householder update, Householder product as u + alpha D[:,q], exact ratio step, one-trip loads and x gather, 3 waves/SIMD and 12 per CU (12,608 B of LDS per wave: the exchange row in R's column 0, Givens parameters in registers), built without machine LICM; gi_box v2.2: lb <= x <= ub, A implicit, dual steepest-edge select with a nonzero key floor, DPP-fused slack and Householder products, one-pass R column shift, 12 waves per CU; gi_wave v6.7 (+ BOX, n <= 32; absent bounds as +inf slacks): x solves with the components captured in LDS (no lane masks, no SGPR spills), dual steepest-edge select with a nonzero key floor, ratio reduction only when a partial step is possible, active A rows for x gathered 16 at a time, DPP-fused sweep, slack product, Householder update and back substitution (no LDS vector reads), Householder product as u + alpha D[:,q], odd-stride R with the exchange row in its column 0 (12 waves per CU), one-trip A gather for x, split setup sweep, 3 waves/SIMD; gi_gram v4.5 (+ BOX, n <= 128: qpb_solve_box with A generated in place) n<=128 on fp64 MFMA, no next-QP prefetch, lane ids opaque per iteration (2 VGPR spills instead of 29), active set as Q1 rows and Z = R^{-1} (parallel passes only), |u|^2 published with the key, broadcast row products, conflict-free diagonal-tile inverses, one-trip loads, cached workspace launched under its lock; ref v6: n <= 1024 (above 128: 1024-thread workgroups, the matrices in a global workspace slice), 64 < n <= 128 one LDS matrix per workgroup (LU, W / V, P in turn), LU rows staged for the solves, branch-free chunked sums)"; }

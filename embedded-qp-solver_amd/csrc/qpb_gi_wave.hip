@@ -640,41 +640,50 @@ __global__ __launch_bounds__(64, OCC) void gi_wave_kernel(
   }
   wave_lds_sync();
   const double invd = ll < n ? rcp(Lp[lrow(ll) + ll]) : 0.0;
-  double acc = gl;
-  double yl = 0.0;
+  // Both solves lane-parallel: step k broadcasts the finished component from
+  // lane k (v_readlane), every lane then updates its own; a lane's entries
+  // past its own component are read unmasked (they sit inside L's packed
+  // storage) and only update dead values, and each component is captured by
+  // a same-address LDS store as it is broadcast (64..95 of the dead R).
+  // Masking those entries instead (kk < ll / kk > ll per step) kept 64 lane
+  // masks live in SGPRs and spilled them (round 6: 112 SGPR spills).
+  double *xcap = R + 2 * NP;
+  double xl;
   {
-    // row ll of L (entries past the diagonal read as zero), then the
-    // lane-parallel forward solve with constant-lane broadcasts
-    double Lrow[NP];
+    double Lrow[NP];  // row ll of L (entries past the diagonal: dead)
     unroll<NP>([&](auto K) {
       constexpr int kk = K;
-      Lrow[kk] = kk < ll ? Lp[lrow(ll) + kk] : 0.0;
+      Lrow[kk] = Lp[lrow(ll) + kk];
     });
+    double acc = gl;
     unroll<NP>([&](auto K) {
       constexpr int kk = K;
       if (kk < n) {
         const double yk = readlane_d(acc * invd, kk);
         acc = __builtin_fma(-Lrow[kk], yk, acc);
+        xcap[kk] = yk;
       }
     });
-    yl = acc * invd;
   }
-  acc = yl;
-  double xl;
+  wave_lds_sync();
   {
-    double Lcol[NP];  // column ll of L below the diagonal
+    double acc = ll < n ? xcap[ll] : 0.0;
+    double Lcol[NP];  // column ll of L (entries above the diagonal: dead)
     unroll<NP>([&](auto K) {
       constexpr int kk = K;
-      Lcol[kk] = (kk > ll && kk < n) ? Lp[lrow(kk) + ll] : 0.0;
+      Lcol[kk] = Lp[lrow(kk) + ll];
     });
+    wave_lds_sync();
     unroll<NP>([&](auto K) {
       constexpr int kk = NP - 1 - K;
       if (kk < n) {
         const double xk = readlane_d(acc * invd, kk);
         acc = __builtin_fma(-Lcol[kk], xk, acc);
+        xcap[kk] = xk;
       }
     });
-    xl = -(acc * invd);
+    wave_lds_sync();
+    xl = -xcap[ll];
   }
   if (status == QPB_OK && wave_any(l < n && !(__builtin_fabs(xl) < kInf))) status = QPB_NUMERICAL;
   clk.tick(10);  // x = -H^{-1} (f + A^T lam)
